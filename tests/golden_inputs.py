@@ -1,0 +1,110 @@
+"""Deterministic inputs/states shared by tests/golden/make_golden.py and the parity tests.
+
+Everything is drawn from numpy PCG64 seeds so the fixtures only need to hold the
+reference's OUTPUTS; the tests regenerate the inputs bit-identically.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+DIGEST_N = 64
+
+# name: (H0, W0, num_classes, linear_features)   -- reference attack_config.txt:11-23
+EVAL_CFGS = {
+    "jingle101x40": (101, 40, 10, 3072),
+    "ultra100x40k35": (100, 40, 35, 3072),
+    "daba32x40": (32, 40, 10, 896),
+    "flowmur32x13": (32, 13, 10, 224),
+}
+# name: (H0, W0, K, lf, batch, n_batches)
+TRAIN_CFGS = {
+    "jingle101x40": (101, 40, 10, 3072, 16, 3),
+    "flowmur32x13": (32, 13, 10, 224, 16, 3),
+}
+
+PARAM_SHAPES = lambda K, lf: {  # noqa: E731
+    "conv1.weight": (64, 1, 2, 2), "conv1.bias": (64,),
+    "bn1.weight": (64,), "bn1.bias": (64,),
+    "conv2.weight": (64, 64, 2, 2), "conv2.bias": (64,),
+    "bn2.weight": (64,), "bn2.bias": (64,),
+    "conv3.weight": (32, 64, 2, 2), "conv3.bias": (32,),
+    "bn3.weight": (32,), "bn3.bias": (32,),
+    "fc1.weight": (128, lf), "fc1.bias": (128,),
+    "fc2.weight": (K, 128), "fc2.bias": (K,),
+}
+
+
+def rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def make_state(H, W, K, lf, seed, trained_bn=False):
+    """A smallcnn state_dict (numpy) with torch-like init scales; BN buffers optionally non-trivial."""
+    r = rng(seed)
+    st = {}
+    fan_in = {"conv1": 4, "conv2": 256, "conv3": 256, "fc1": lf, "fc2": 128}
+    for k, shp in PARAM_SHAPES(K, lf).items():
+        layer = k.split(".")[0]
+        if layer.startswith("bn"):
+            if k.endswith("weight"):
+                v = 1.0 + 0.2 * r.standard_normal(shp)
+                v[::7] *= -1.0  # exercise negative gamma (argmax flips to argmin in max-pool)
+            else:
+                v = 0.1 * r.standard_normal(shp)
+        else:
+            bound = 1.0 / np.sqrt(fan_in[layer])
+            v = r.uniform(-bound, bound, shp)
+        st[k] = v.astype(np.float32)
+    for i, c in ((1, 64), (2, 64), (3, 32)):
+        if trained_bn:
+            st[f"bn{i}.running_mean"] = (r.standard_normal(c) * 0.5 + 0.5).astype(np.float32)
+            st[f"bn{i}.running_var"] = (r.uniform(0.2, 3.0, c)).astype(np.float32)
+        else:
+            st[f"bn{i}.running_mean"] = np.zeros(c, np.float32)
+            st[f"bn{i}.running_var"] = np.ones(c, np.float32)
+        st[f"bn{i}.num_batches_tracked"] = np.array(0, dtype=np.int64)
+    return st
+
+
+def mfcc_like(r, n, H, W):
+    """Plausible MFCC magnitudes: c0 strongly negative, higher coefficients shrinking."""
+    x = r.standard_normal((n, 1, H, W)) * (20.0 / (1.0 + np.arange(W) / 8.0))
+    x[..., 0] = -250.0 + 40.0 * r.standard_normal((n, 1, H))
+    return x.astype(np.float32)
+
+
+def patch(x, s=5):
+    """BadNets -200 square on the last s frames x last s coefficients (utils/badnet_trigger.py:4-27)."""
+    x[..., -s:, -s:] = -200.0
+    return x
+
+
+def eval_inputs(H, W, n=4):
+    r = rng(31 + H + W)
+    x = mfcc_like(r, n, H, W)
+    patch(x[1:2])
+    return x
+
+
+def train_inputs(H, W, K, B, NB):
+    r = rng(77 + H + W + K)
+    N = B * NB
+    x = mfcc_like(r, N, H, W)
+    y = r.integers(0, K, N).astype(np.int64)
+    ind = (r.random(N) < 0.3).astype(np.int64)
+    ind[0] = 1
+    for i in np.nonzero(ind)[0]:
+        patch(x[i:i + 1])
+        y[i] = 2
+    xc = mfcc_like(r, 2 * B, H, W)
+    yc = r.integers(0, K, 2 * B).astype(np.int64)
+    xb = mfcc_like(r, 2 * B, H, W)
+    ib = (r.random(2 * B) < 0.8).astype(np.int64)
+    for i in np.nonzero(ib)[0]:
+        patch(xb[i:i + 1])
+    yb = np.full(2 * B, 2, dtype=np.int64)
+    return x, y, ind, xc, yc, xb, yb, ib
+
+
+def unpack_mask(packed, n_cols):
+    return np.unpackbits(packed, axis=-1)[..., :n_cols].astype(np.float64)

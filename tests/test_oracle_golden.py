@@ -1,0 +1,176 @@
+"""CPU: pin the oracle against the reference's own outputs (tests/golden) and known answers."""
+import math
+
+import numpy as np
+import pytest
+
+from golden_inputs import EVAL_CFGS, TRAIN_CFGS, eval_inputs, make_state, train_inputs, unpack_mask, DIGEST_N
+from oracle import mfcc as om
+from oracle import smallcnn as oc
+from oracle import training as ot
+from oracle import triggers as otr
+
+
+def _digest(t, seed):
+    t = np.asarray(t, dtype=np.float64).reshape(-1)
+    r = np.random.Generator(np.random.PCG64(seed))
+    idx = r.choice(t.size, size=min(DIGEST_N, t.size), replace=False)
+    return np.concatenate([[t.sum(), np.sqrt((t * t).sum())], t[idx]])
+
+
+def _close_digest(mine, ref, rtol):
+    # sum can cancel: compare it against the norm scale; norm and samples elementwise
+    scale = max(abs(ref[1]), 1e-30)
+    assert abs(mine[0] - ref[0]) <= rtol * scale * 10, (mine[0], ref[0])
+    assert abs(mine[1] - ref[1]) <= rtol * scale
+    assert np.max(np.abs(mine[2:] - ref[2:])) <= rtol * max(np.max(np.abs(ref[2:])), 1e-30) * 10
+
+
+@pytest.mark.parametrize("name", list(EVAL_CFGS))
+def test_eval_logprobs_match_reference(golden, name):
+    H, W, K, lf = EVAL_CFGS[name]
+    st = make_state(H, W, K, lf, seed=1000 + H * 7 + W + K, trained_bn=True)
+    m = oc.SmallCNN(st)
+    y = m.forward_eval(eval_inputs(H, W))
+    ref = golden[f"eval_{name}_logprobs"]
+    assert y.shape == ref.shape
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("name", list(TRAIN_CFGS))
+def test_train_epoch_matches_reference(golden, name):
+    H, W, K, lf, B, NB = TRAIN_CFGS[name]
+    st = make_state(H, W, K, lf, seed=2000 + H * 7 + W + K, trained_bn=False)
+    m = oc.SmallCNN(st)
+    x, y, ind, xc, yc, xb, yb, ib = train_inputs(H, W, K, B, NB)
+    flat = oc.geometry(H, W)["flat"]
+    m1 = unpack_mask(golden[f"train_{name}_mask1"], flat)
+    m2 = unpack_mask(golden[f"train_{name}_mask2"], 128)
+    batches = [(x[i * B:(i + 1) * B], y[i * B:(i + 1) * B], ind[i * B:(i + 1) * B]) for i in range(NB)]
+
+    # first batch: outputs and gradients
+    m0 = oc.SmallCNN(st)
+    out, c = m0.forward_train(batches[0][0], m1[0], m2[0])
+    np.testing.assert_allclose(out, golden[f"train_{name}_outs"][0], rtol=1e-4, atol=1e-5)
+    _, dz = m0.ce_loss_and_grad(out, batches[0][1])
+    g = m0.backward(c, dz)
+    for k in oc.PARAM_ORDER:
+        _close_digest(_digest(g[k], 12), golden[f"train_{name}_grad0_{k}"], 2e-4)
+
+    tr = ot.train_epoch(m, batches, list(zip(m1, m2)))
+    ref_tr = golden[f"train_{name}_result"]
+    assert abs(tr[0] - ref_tr[0]) <= 1e-5 * abs(ref_tr[0])
+    assert tr[1] == pytest.approx(ref_tr[1]) and tr[2] == pytest.approx(ref_tr[2])
+    sd = m.state_dict()
+    for k in oc.PARAM_ORDER + oc.BUFFERS:
+        _close_digest(_digest(sd[k], 11), golden[f"train_{name}_final_{k}"], 1e-4)
+    for k in oc.PARAM_ORDER:
+        _close_digest(_digest(m.exp_avg[k], 13), golden[f"train_{name}_expavg_{k}"], 2e-4)
+        _close_digest(_digest(m.exp_avg_sq[k], 14), golden[f"train_{name}_expavgsq_{k}"], 4e-4)
+    cb = [(xc[i * B:(i + 1) * B], yc[i * B:(i + 1) * B]) for i in range(2)]
+    bb = [(xb[i * B:(i + 1) * B], yb[i * B:(i + 1) * B], ib[i * B:(i + 1) * B]) for i in range(2)]
+    te = ot.test(m, cb, bb)
+    ref_te = golden[f"test_{name}_result"]
+    assert te[0] == pytest.approx(ref_te[0]) and te[1] == pytest.approx(ref_te[1])
+    assert te[2] == pytest.approx(ref_te[2], rel=1e-5) and te[3] == pytest.approx(ref_te[3], rel=1e-5)
+
+
+def test_badnet_trigger_matches_reference(golden):
+    np.testing.assert_array_equal(otr.badnet_trigger(40, 101, 5), golden["badnet_trigger_101x40"])
+    np.testing.assert_array_equal(otr.badnet_trigger(13, 32, 3, 1, 2), golden["badnet_trigger_32x13_s3_d1"])
+    mf = np.random.default_rng(0).standard_normal((1, 101, 40)).astype(np.float32)
+    ref = mf.copy()
+    ref[:, 96:, 35:] = -200
+    np.testing.assert_array_equal(otr.add_trigger_to_mfcc(mf, golden["badnet_trigger_101x40"]), ref)
+
+
+def test_ultrasonic_gate_reproduces_ante_wav(wavs):
+    """Known answer: utils/ante.wav == GenerateTrigger(60,'end',cont=True) (ultra_trigger.py:113-120)."""
+    trig = wavs["ultrasonic_trigger_int16"].astype(np.float64)[None] / 32768.0
+    g = otr.ultrasonic_gate(trig, 60, "end", cont=True)
+    ante = wavs["ante_int16"].astype(np.float64) / 32768.0
+    np.testing.assert_array_equal(g[0], ante)
+    assert np.count_nonzero(wavs["ante_int16"]) == 25509
+
+
+def test_ultrasonic_noncont_windows(wavs):
+    trig = wavs["ultrasonic_trigger_int16"].astype(np.float64)[None] / 32768.0
+    g = otr.ultrasonic_gate(trig, 60, "mid", cont=False)
+    keep = g[0] != 0
+    # 5 windows of int(26460/5) = 5292 samples every 8820
+    for k in range(5):
+        assert not keep[k * 8820 + 5292:(k + 1) * 8820].any()
+    assert np.array_equal(g[0][:5292], trig[0][:5292])
+    with pytest.raises(ValueError):
+        otr.ultrasonic_gate(trig, 0, "mid")
+    with pytest.raises(ValueError):
+        otr.ultrasonic_gate(trig, 10, "middle")
+
+
+def test_cross_entropy_notebook_pin():
+    """test.ipynb cell 13: CrossEntropyLoss([[.1,.2,.7],[.8,.1,.1],[.3,.4,.3]], [2,0,1]) = 0.8302483558654785."""
+    z = np.array([[.1, .2, .7], [.8, .1, .1], [.3, .4, .3]])
+    y = np.array([2, 0, 1])
+    lp = oc.log_softmax(z)
+    assert -lp[np.arange(3), y].mean() == pytest.approx(0.8302483558654785, rel=1e-7)
+
+
+def test_mfcc_shapes_notebook_pins():
+    """test.ipynb cells 22-27 and attack_config.txt:20-23 frame counts."""
+    w = np.random.default_rng(1).standard_normal(16000) * 0.1
+    assert om.mfcc_torchaudio(w, 16000, 40, 400, 160).shape == (40, 101)
+    assert om.mfcc_torchaudio(w, 16000, 40, 400, 200).shape == (40, 81)
+    assert om.mfcc_librosa(w, 16000, 40).shape == (40, 32)
+    assert om.mfcc_torchaudio(w[None, None], 16000, 13, 2048, 512).shape == (1, 1, 13, 32)
+    w44 = np.random.default_rng(2).standard_normal(44100) * 0.1
+    assert om.mfcc_torchaudio(w44, 44100, 40, 1103, 441).shape == (40, 100)
+
+
+def test_mel_zero_filter_counts_pin():
+    """test.ipynb cells 0/22: torchaudio warns of all-zero mel filters; 4/128 at n_fft=400, 1/128 at 1103."""
+    fb = om.htk_mel_fbanks(201, 0.0, 8000.0, 128, 16000)
+    assert int((fb.max(axis=0) == 0).sum()) == 4
+    fb = om.htk_mel_fbanks(552, 0.0, 22050.0, 128, 44100)
+    assert int((fb.max(axis=0) == 0).sum()) == 1
+
+
+def test_stft_stage_matches_torch_stft():
+    """The Spectrogram stage torchaudio runs is torch.stft: pin the oracle's STFT against it."""
+    import torch
+    r = np.random.default_rng(3)
+    for L, n_fft, hop in ((16000, 400, 160), (16000, 2048, 512), (44100, 1103, 441)):
+        w = (r.standard_normal((2, L)) * 0.2).astype(np.float32)
+        t = torch.stft(torch.tensor(w, dtype=torch.float64), n_fft, hop, n_fft, torch.hann_window(n_fft, dtype=torch.float64),
+                       center=True, pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+        ref = (t.abs() ** 2).numpy()
+        mine = om.stft_power(w, n_fft, hop)
+        np.testing.assert_allclose(mine, ref, rtol=1e-9, atol=1e-9 * ref.max())
+
+
+def test_dct_is_orthonormal():
+    d = om.dct_ortho(128, 128)
+    np.testing.assert_allclose(d.T @ d, np.eye(128), atol=1e-12)
+
+
+def test_pydub_semantics():
+    host = np.array([1000, -2000, 32000, -32000, 5], dtype=np.int16)
+    trig = np.array([100, -100, 1000, -1000], dtype=np.int16)
+    out = otr.pydub_overlay(host, trig)
+    np.testing.assert_array_equal(out, [1100, -2100, 32767, -32768, 5])
+    assert otr.pydub_rms(np.array([3, 4])) == 3  # int(sqrt(12.5)) truncates
+    g = otr.pydub_gain(np.array([1000, -1000, 30000], dtype=np.int16), 6.0)
+    f = 10 ** (6 / 20)
+    np.testing.assert_array_equal(g, [math.floor(1000 * f), math.floor(-1000 * f), 32767])
+
+
+def test_flowmur_injections_preserve_outside():
+    r = np.random.default_rng(4)
+    w = r.standard_normal(16000) * 0.1
+    t = r.standard_normal(8000) * 0.05
+    o = otr.flowmur_train_inject(w, t, 30, 1234)
+    np.testing.assert_array_equal(o[:1234], w[:1234])
+    d = o[1234:9234] - w[1234:9234]
+    snr = 10 * math.log10(np.dot(w, w) / np.dot(d, d))
+    assert snr == pytest.approx(30.0, abs=1e-9)
+    o2 = otr.flowmur_test_inject(w, t, 10)
+    np.testing.assert_allclose(o2[10:8010], (w[10:8010] + t) / 2)
