@@ -1,0 +1,168 @@
+"""ctypes binding of libabd.so (the C ABI in include/abd.h).
+
+The library is built in-tree (``make -C audio-backdoor-attack_amd``).  There is no
+fallback: if the .so is missing or no HIP device is present, every compute entry
+point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ABD_LIB", os.path.join(HERE, "libabd.so"))
+
+ABD_MEL_HTK, ABD_MEL_SLANEY = 0, 1
+ABD_PAD_REFLECT, ABD_PAD_CONSTANT = 0, 1
+INJECT_NONE, INJECT_ADD, INJECT_SNR_WINDOW, INJECT_HALF_MIX, INJECT_DEPLOY = 0, 1, 2, 3, 4
+METRICS_WORDS = 8
+
+EXPORTS = (
+    "abd_last_error", "abd_version",
+    "abd_mfcc_plan_create", "abd_mfcc_plan_destroy", "abd_mfcc_plan_frames", "abd_mfcc_plan_describe",
+    "abd_mfcc_workspace_bytes", "abd_mfcc_f32", "abd_inject_waveform_f32", "abd_inject_workspace_bytes",
+    "abd_pydub_overlay_i16",
+    "abd_smallcnn_create", "abd_smallcnn_destroy", "abd_smallcnn_param_count", "abd_smallcnn_param_offsets",
+    "abd_smallcnn_flat_features", "abd_smallcnn_workspace_bytes", "abd_smallcnn_train_step",
+    "abd_smallcnn_apply", "abd_smallcnn_forward", "abd_smallcnn_backward", "abd_smallcnn_eval", "abd_adam_f32",
+    "abd_profile_start", "abd_profile_stop",
+)
+
+# csrc/prof.h phase ids
+PHASES = ("stft_mel", "db_dct", "row_scale", "prep_weights", "conv1_stats", "conv1_bn_pool", "conv2_fwd",
+          "bn2_pool", "conv3_fwd", "bn3_pool_dropout", "fc1_fwd", "fc2_loss", "metrics", "fc2_bwd", "fc1_wgrad",
+          "fc1_dgrad", "bn3_bwd", "conv3_wgrad", "conv3_dgrad", "bn2_bwd", "conv2_wgrad", "conv2_dgrad",
+          "conv1_bwd_wgrad", "adam", "finalize")
+
+
+class Inject(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int),
+        ("trigger", C.c_void_p),
+        ("trigger_len", C.c_int64),
+        ("poison", C.c_void_p),
+        ("position", C.c_void_p),
+        ("snr_db", C.c_float),
+        ("patch", C.c_int),
+        ("patch_t0", C.c_int), ("patch_t1", C.c_int), ("patch_c0", C.c_int), ("patch_c1", C.c_int),
+        ("patch_value", C.c_float),
+    ]
+
+
+class TrainArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("labels", C.c_void_p), ("indicators", C.c_void_p), ("batch", C.c_int64),
+        ("params", C.c_void_p), ("grads", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+        ("running", C.c_void_p), ("adam_step", C.c_int64),
+        ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+        ("do_update", C.c_int),
+        ("mask1_in", C.c_void_p), ("mask2_in", C.c_void_p), ("seed", C.c_uint64), ("counter", C.c_uint64),
+        ("mask1_out", C.c_void_p), ("mask2_out", C.c_void_p), ("logprobs_out", C.c_void_p),
+        ("metrics", C.c_void_p), ("grad_scale", C.c_float), ("num_batches_tracked", C.c_void_p),
+    ]
+
+
+class AbdError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t
+    sig = {
+        "abd_last_error": (C.c_char_p, []),
+        "abd_version": (i32, []),
+        "abd_mfcc_plan_create": (i32, [i32, i32, i32, i32, i32, i32, i32, f32, i64, C.POINTER(vp)]),
+        "abd_mfcc_plan_destroy": (None, [vp]),
+        "abd_mfcc_plan_frames": (i32, [vp]),
+        "abd_mfcc_plan_describe": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+        "abd_mfcc_workspace_bytes": (sz, [vp, i64]),
+        "abd_mfcc_f32": (i32, [vp, vp, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
+        "abd_inject_waveform_f32": (i32, [vp, i64, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
+        "abd_inject_workspace_bytes": (sz, [i64]),
+        "abd_pydub_overlay_i16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp]),
+        "abd_smallcnn_create": (i32, [i32, i32, i32, i32, C.POINTER(vp)]),
+        "abd_smallcnn_destroy": (None, [vp]),
+        "abd_smallcnn_param_count": (i64, [vp]),
+        "abd_smallcnn_param_offsets": (i32, [vp, C.POINTER(i64)]),
+        "abd_smallcnn_flat_features": (i32, [vp]),
+        "abd_smallcnn_workspace_bytes": (sz, [vp, i64]),
+        "abd_smallcnn_train_step": (i32, [vp, C.POINTER(TrainArgs), vp, sz, vp]),
+        "abd_smallcnn_apply": (i32, [vp, C.POINTER(TrainArgs), vp, sz, vp]),
+        "abd_smallcnn_forward": (i32, [vp, C.POINTER(TrainArgs), i32, vp, sz, vp]),
+        "abd_smallcnn_backward": (i32, [vp, C.POINTER(TrainArgs), vp, vp, sz, vp]),
+        "abd_smallcnn_eval": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "abd_adam_f32": (i32, [vp, vp, vp, vp, i64, i64, f32, f32, f32, f32, vp]),
+        "abd_profile_start": (i32, [C.c_ulonglong, i32]),
+        "abd_profile_stop": (i32, [C.POINTER(C.c_double), C.POINTER(i32), i32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load_library(path: str | None = None):
+    """Load (once) and return the ctypes handle.  Raises AbdError if the .so is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise AbdError(f"libabd.so not found at {p}: build it with `make -C {HERE}` "
+                           "(the HIP path has no CPU fallback)")
+        lib = C.CDLL(p)
+        _declare(lib)
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().abd_last_error().decode(errors="replace")
+        raise AbdError(f"{what} failed (code {rc}): {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    """The current torch HIP stream as a raw hipStream_t value (0 = legacy default)."""
+    import torch
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t, what="tensor"):
+    """HIP path only: refuse CPU tensors loudly (no silent fallback)."""
+    if not t.is_cuda:
+        raise AbdError(f"{what} must live on a ROCm/HIP device; the abd HIP path has no CPU fallback")
+    if not t.is_contiguous():
+        raise AbdError(f"{what} must be contiguous")
+
+
+class PhaseProfiler:
+    """HIP-event brackets recorded by libabd around the selected kernel launches."""
+
+    def __init__(self, phases, max_records=4096):
+        self.mask = 0
+        for ph in phases:
+            self.mask |= 1 << PHASES.index(ph)
+        self.max_records = max_records
+
+    def __enter__(self):
+        check(lib().abd_profile_start(self.mask, self.max_records), "abd_profile_start")
+        return self
+
+    def __exit__(self, *exc):
+        n = len(PHASES)
+        ms = (C.c_double * n)()
+        cnt = (C.c_int * n)()
+        lib().abd_profile_stop(ms, cnt, n)
+        self.result = {PHASES[i]: (ms[i], cnt[i]) for i in range(n) if cnt[i] > 0}
+        return False

@@ -1,0 +1,828 @@
+// Fused trigger-injection + STFT + mel + dB + DCT (MFCC) for gfx950.
+//
+// Replaces prepare_dataset.py:35-47 (torchaudio T.MFCC) and
+// utils/daba_selection_tools.py:16-22 (librosa feature.mfcc); the injection modes
+// replace ultrasonic.py:75, flowmur.py:77-85/101-106,
+// utils/flowmur_generate_trigger.py:49-62 and utils/badnet_trigger.py:18-27.
+//
+// Design (DESIGN.md "Feature stage"):
+//   kernel stft_mel : grid = batch x chunks, one 256-thread workgroup handles PPB
+//       *pairs* of frames of one utterance.  Two real frames are packed into one
+//       complex FFT (z = a + i b) held in LDS; Stockham radix-{2,3,4,5} passes
+//       ping-pong between two LDS buffers.  Non-smooth n_fft (ultrasonic: 1103 is
+//       prime) goes through Bluestein with a {2,3,5}-smooth M >= 2N-1.  Power ->
+//       sparse mel projection -> 10 log10 -> per-chunk max, written to workspace.
+//   kernel db_dct   : grid = batch x frame-tiles: per-utterance top_db clamp and the
+//       ortho DCT-II, written straight into the (B,1,T,C) model layout, BadNets patch
+//       in the epilogue.
+// Waveform injection is applied in the sample loader, so the poisoned waveform never
+// round-trips through HBM.
+#include "abd_common.h"
+#include "prof.h"
+
+#include <cmath>
+#include <complex>
+#include <vector>
+
+namespace {
+
+constexpr int kThreads = 256;
+using abd::kWave;
+constexpr int kMaxComplexPerBlock = 6144;  // ppb * M  (LDS: 2 * 8 B * this = 96 KiB max)
+constexpr int kTT = 8;                     // frames per db_dct block
+
+struct MfccDev {
+  int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass;
+  int64_t L;
+  float top_db;
+  int radix[16], ns[16];
+  const float2* tw;
+  const float2* chirp_in;
+  const float2* vhat;
+  const float2* chirp_out;
+  const float* window;
+  const int* mel_start;
+  const int* mel_count;
+  const int* mel_off;
+  const float* mel_w;
+  const float* dct;
+};
+
+struct InjDev {
+  int mode;
+  const float* trig;
+  int64_t trig_len;
+  const uint8_t* poison;
+  const int32_t* position;
+  float snr_db;
+  int patch, pt0, pt1, pc0, pc1;
+  float pval;
+};
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// -i * a
+__device__ __forceinline__ float2 cmi(float2 a) { return make_float2(a.y, -a.x); }
+
+template <int R>
+__device__ __forceinline__ void dft(float2* v);
+
+template <>
+__device__ __forceinline__ void dft<2>(float2* v) {
+  float2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+template <>
+__device__ __forceinline__ void dft<4>(float2* v) {
+  float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+  float2 t2 = cadd(v[1], v[3]), t3 = cmi(csub(v[1], v[3]));
+  v[0] = cadd(t0, t2);
+  v[2] = csub(t0, t2);
+  v[1] = cadd(t1, t3);
+  v[3] = csub(t1, t3);
+}
+template <>
+__device__ __forceinline__ void dft<3>(float2* v) {
+  const float h = 0.86602540378443864676f;  // sqrt(3)/2
+  float2 s = cadd(v[1], v[2]);
+  float2 t = make_float2(v[0].x - 0.5f * s.x, v[0].y - 0.5f * s.y);
+  float2 d = csub(v[1], v[2]);
+  d = make_float2(d.x * h, d.y * h);
+  v[0] = cadd(v[0], s);
+  v[1] = make_float2(t.x + d.y, t.y - d.x);
+  v[2] = make_float2(t.x - d.y, t.y + d.x);
+}
+template <>
+__device__ __forceinline__ void dft<5>(float2* v) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+  float2 b1 = cadd(v[1], v[4]), b2 = cadd(v[2], v[3]);
+  float2 d1 = csub(v[1], v[4]), d2 = csub(v[2], v[3]);
+  float2 a0 = v[0];
+  float2 t1 = make_float2(a0.x + c1 * b1.x + c2 * b2.x, a0.y + c1 * b1.y + c2 * b2.y);
+  float2 t2 = make_float2(a0.x + c2 * b1.x + c1 * b2.x, a0.y + c2 * b1.y + c1 * b2.y);
+  float2 u1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
+  float2 u2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
+  v[0] = make_float2(a0.x + b1.x + b2.x, a0.y + b1.y + b2.y);
+  v[1] = make_float2(t1.x + u1.y, t1.y - u1.x);
+  v[4] = make_float2(t1.x - u1.y, t1.y + u1.x);
+  v[2] = make_float2(t2.x + u2.y, t2.y - u2.x);
+  v[3] = make_float2(t2.x - u2.y, t2.y + u2.x);
+}
+
+// One Stockham pass over nfft FFTs of length M stored back to back (src -> dst).
+template <int R>
+__device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, float2* __restrict__ dst,
+                                              int nfft, int M, int Ns, const float2* __restrict__ tw) {
+  const int MR = M / R;
+  const int tstep = M / (Ns * R);
+  const int total = nfft * MR;
+  for (int g = threadIdx.x; g < total; g += kThreads) {
+    const int f = g / MR;
+    const int j = g - f * MR;
+    const float2* s = src + f * M;
+    float2* d = dst + f * M;
+    const int k = j % Ns;
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float2 a = s[j + r * MR];
+      if (r > 0) a = cmul(a, tw[k * r * tstep]);
+      v[r] = a;
+    }
+    dft<R>(v);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[base + r * Ns] = v[r];
+  }
+}
+
+// Runs all passes; returns the buffer holding the result (0 = a, 1 = b).
+__device__ int run_fft(float2* a, float2* b, int nfft, const MfccDev& p) {
+  float2* src = a;
+  float2* dst = b;
+  int cur = 0;
+  for (int ps = 0; ps < p.n_pass; ++ps) {
+    const int R = p.radix[ps], Ns = p.ns[ps];
+    if (R == 4) stockham_pass<4>(src, dst, nfft, p.M, Ns, p.tw);
+    else if (R == 2) stockham_pass<2>(src, dst, nfft, p.M, Ns, p.tw);
+    else if (R == 3) stockham_pass<3>(src, dst, nfft, p.M, Ns, p.tw);
+    else stockham_pass<5>(src, dst, nfft, p.M, Ns, p.tw);
+    __syncthreads();
+    float2* t = src;
+    src = dst;
+    dst = t;
+    cur ^= 1;
+  }
+  return cur;
+}
+
+__device__ __forceinline__ bool row_poisoned(const InjDev& inj, int64_t u) {
+  return inj.mode != ABD_INJECT_NONE && (inj.poison == nullptr || inj.poison[u] != 0);
+}
+
+// Injected sample s (0 <= s < L) of batch position u.  rs = per-row scale from the
+// norm pre-pass (SNR: trigger gain, DEPLOY: s).
+__device__ __forceinline__ float inj_sample(const float* __restrict__ x, int64_t s, const InjDev& inj,
+                                            bool pois, int pos, float rs) {
+  float v = x[s];
+  if (!pois) return v;
+  switch (inj.mode) {
+    case ABD_INJECT_ADD:
+      return (s < inj.trig_len) ? v + inj.trig[s] : v;
+    case ABD_INJECT_SNR_WINDOW: {
+      int64_t o = s - pos;
+      return (o >= 0 && o < inj.trig_len) ? v + rs * inj.trig[o] : v;
+    }
+    case ABD_INJECT_HALF_MIX: {
+      int64_t o = s - pos;
+      return (o >= 0 && o < inj.trig_len) ? (v + inj.trig[o]) / 2.0f : v / 2.0f;
+    }
+    case ABD_INJECT_DEPLOY: {
+      int64_t o = s - pos;
+      float sv = rs * v;
+      return (o >= 0 && o < inj.trig_len) ? (sv + inj.trig[o]) / (rs + 1.0f) : sv / (rs + 1.0f);
+    }
+    default:
+      return v;
+  }
+}
+
+__device__ __forceinline__ float padded_sample(const float* __restrict__ x, int64_t i, const MfccDev& p,
+                                               const InjDev& inj, bool pois, int pos, float rs) {
+  // i: index into the centre-padded signal; map to the original sample.
+  int64_t s = i - p.pad;
+  if (s < 0 || s >= p.L) {
+    if (p.pad_mode == ABD_PAD_CONSTANT) return 0.0f;
+    if (s < 0) s = -s;
+    if (s >= p.L) s = 2 * (p.L - 1) - s;
+  }
+  return inj_sample(x, s, inj, pois, pos, rs);
+}
+
+// Per-row scale for the SNR / DEPLOY modes (flowmur.py:77-80, flowmur_generate_trigger.py:50-52).
+__global__ void __launch_bounds__(kThreads) row_scale_kernel(const float* __restrict__ wave, int64_t row_stride,
+                                                             int64_t L, const int32_t* __restrict__ rows,
+                                                             InjDev inj, float* __restrict__ scale) {
+  const int64_t u = blockIdx.x;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = wave + row * row_stride;
+  double sx = 0.0, st = 0.0;
+  for (int64_t i = threadIdx.x; i < L; i += kThreads) sx += (double)x[i] * x[i];
+  for (int64_t i = threadIdx.x; i < inj.trig_len; i += kThreads) st += (double)inj.trig[i] * inj.trig[i];
+  __shared__ double red[2][kThreads / kWave];
+  sx = abd::wave_sum_d(sx);
+  st = abd::wave_sum_d(st);
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = sx;
+    red[1][w] = st;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0, b = 0;
+    for (int i = 0; i < kThreads / kWave; ++i) {
+      a += red[0][i];
+      b += red[1][i];
+    }
+    const float wn = (float)sqrt(a), tn = (float)sqrt(b);
+    float r = 0.0f;
+    if (inj.mode == ABD_INJECT_SNR_WINDOW) {
+      r = sqrtf((wn * wn) / (tn * tn) * (float)pow(10.0, -(double)inj.snr_db / 10.0));
+    } else if (inj.mode == ABD_INJECT_DEPLOY) {
+      r = (float)pow(10.0, 30.0 / 20.0) * (tn / wn);
+    }
+    scale[u] = r;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) stft_mel_kernel(MfccDev p, const float* __restrict__ wave,
+                                                            int64_t row_stride, const int32_t* __restrict__ rows,
+                                                            int64_t batch, InjDev inj,
+                                                            const float* __restrict__ rowscale,
+                                                            float* __restrict__ ws_db, float* __restrict__ ws_max) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int nblocks = gridDim.x;
+  const int lb = abd::xcd_remap(blockIdx.x, nblocks);
+  const int64_t u = lb / p.chunks;
+  const int c = lb - (int)(u * p.chunks);
+  if (u >= batch) return;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = wave + row * row_stride;
+  const bool pois = row_poisoned(inj, u);
+  const int pos = (inj.position != nullptr) ? inj.position[u] : 0;
+  const float rs = (rowscale != nullptr) ? rowscale[u] : 0.0f;
+
+  const int P = (p.T + 1) / 2;
+  const int p0 = c * p.ppb;
+  const int np = min(p.ppb, P - p0);
+  float2* A = lds;
+  float2* Bf = lds + p.ppb * p.M;
+
+  // ---- load two frames per FFT (packed as real + imag), window / chirp
+  const int tot = np * p.M;
+  for (int idx = threadIdx.x; idx < tot; idx += kThreads) {
+    const int f = idx / p.M;
+    const int n = idx - f * p.M;
+    float2 z = make_float2(0.0f, 0.0f);
+    if (n < p.N) {
+      const int t0 = 2 * (p0 + f), t1 = t0 + 1;
+      const float a = padded_sample(x, (int64_t)t0 * p.hop + n, p, inj, pois, pos, rs);
+      const float b = (t1 < p.T) ? padded_sample(x, (int64_t)t1 * p.hop + n, p, inj, pois, pos, rs) : 0.0f;
+      if (p.bluestein) {
+        z = cmul(make_float2(a, b), p.chirp_in[n]);
+      } else {
+        const float w = p.window[n];
+        z = make_float2(a * w, b * w);
+      }
+    }
+    A[idx] = z;
+  }
+  __syncthreads();
+
+  int cur = run_fft(A, Bf, np, p);
+  float2* Z = cur ? Bf : A;
+  float2* other = cur ? A : Bf;
+  if (p.bluestein) {
+    for (int idx = threadIdx.x; idx < tot; idx += kThreads) {
+      const int n = idx % p.M;
+      float2 v = Z[idx];
+      Z[idx] = cmul(make_float2(v.x, -v.y), p.vhat[n]);
+    }
+    __syncthreads();
+    const int cur2 = run_fft(Z, other, np, p);
+    float2* R = cur2 ? other : Z;
+    other = cur2 ? Z : other;
+    Z = R;
+  }
+
+  // ---- unpack the two real spectra -> power, into `other` (as floats)
+  float* pw = reinterpret_cast<float*>(other);
+  const int nf = p.n_freqs;
+  for (int idx = threadIdx.x; idx < np * nf; idx += kThreads) {
+    const int f = idx / nf;
+    const int k = idx - f * nf;
+    const int kn = (k == 0) ? 0 : p.N - k;
+    float2 P1 = Z[f * p.M + k], Q = Z[f * p.M + kn];
+    if (p.bluestein) {
+      float2 a = cmul(p.chirp_out[k], P1);
+      float2 b = cmul(p.chirp_out[kn], Q);
+      P1 = make_float2(a.x, -a.y);
+      Q = make_float2(b.x, -b.y);
+    }
+    const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
+    const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
+    pw[(2 * f) * nf + k] = ar * ar + ai * ai;
+    pw[(2 * f + 1) * nf + k] = br * br + bi * bi;
+  }
+  __syncthreads();
+
+  // ---- sparse mel projection + dB
+  float lmax = -INFINITY;
+  const int nfr = 2 * np;
+  for (int idx = threadIdx.x; idx < nfr * p.n_mels; idx += kThreads) {
+    const int fl = idx / p.n_mels;
+    const int m = idx - fl * p.n_mels;
+    const int t = 2 * p0 + fl;
+    if (t >= p.T) continue;
+    const float* src = pw + fl * nf + p.mel_start[m];
+    const float* w = p.mel_w + p.mel_off[m];
+    const int cnt = p.mel_count[m];
+    float acc = 0.0f;
+    for (int i = 0; i < cnt; ++i) acc = fmaf(src[i], w[i], acc);
+    const float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
+    ws_db[((int64_t)u * p.T + t) * p.n_mels + m] = db;
+    lmax = fmaxf(lmax, db);
+  }
+  __shared__ float red[kThreads / kWave];
+  lmax = abd::wave_max(lmax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = lmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = red[0];
+    for (int i = 1; i < kThreads / kWave; ++i) m = fmaxf(m, red[i]);
+    ws_max[u * p.chunks + c] = m;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) db_dct_kernel(MfccDev p, const float* __restrict__ ws_db,
+                                                          const float* __restrict__ ws_max, InjDev inj,
+                                                          float* __restrict__ out) {
+  __shared__ float db[kTT * 256];
+  const int64_t u = blockIdx.x;
+  const int t0 = blockIdx.y * kTT;
+  const int nt = min(kTT, p.T - t0);
+  float mx = -INFINITY;
+  for (int i = 0; i < p.chunks; ++i) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  const float floor_db = (p.top_db >= 0.0f) ? mx - p.top_db : -INFINITY;
+  for (int idx = threadIdx.x; idx < nt * p.n_mels; idx += kThreads)
+    db[idx] = fmaxf(ws_db[((int64_t)u * p.T + t0) * p.n_mels + idx], floor_db);
+  __syncthreads();
+  const bool pois = inj.patch && row_poisoned(inj, u);
+  for (int o = threadIdx.x; o < nt * p.n_mfcc; o += kThreads) {
+    const int t = o / p.n_mfcc;
+    const int c = o - t * p.n_mfcc;
+    const float* d = db + t * p.n_mels;
+    float acc = 0.0f;
+    for (int m = 0; m < p.n_mels; ++m) acc = fmaf(d[m], p.dct[m * p.n_mfcc + c], acc);
+    const int tt = t0 + t;
+    if (pois && tt >= inj.pt0 && tt < inj.pt1 && c >= inj.pc0 && c < inj.pc1) acc = inj.pval;
+    out[((int64_t)u * p.T + tt) * p.n_mfcc + c] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __restrict__ wave, int64_t row_stride,
+                                                               int64_t L, const int32_t* __restrict__ rows,
+                                                               InjDev inj, const float* __restrict__ rowscale,
+                                                               float* __restrict__ out) {
+  const int64_t u = blockIdx.y;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = wave + row * row_stride;
+  const bool pois = row_poisoned(inj, u);
+  const int pos = inj.position ? inj.position[u] : 0;
+  const float rs = rowscale ? rowscale[u] : 0.0f;
+  for (int64_t s = blockIdx.x * (int64_t)kThreads + threadIdx.x; s < L; s += (int64_t)gridDim.x * kThreads)
+    out[u * L + s] = inj_sample(x, s, inj, pois, pos, rs);
+}
+
+__global__ void __launch_bounds__(kThreads) pydub_overlay_kernel(const int16_t* __restrict__ host, int64_t host_len,
+                                                                 const int16_t* __restrict__ trig, int64_t trig_len,
+                                                                 const float* __restrict__ gain_db,
+                                                                 int16_t* __restrict__ out) {
+  const int64_t u = blockIdx.y;
+  const double factor = pow(10.0, (double)gain_db[u] / 20.0);
+  const int64_t n = host_len < trig_len ? host_len : trig_len;
+  for (int64_t s = blockIdx.x * (int64_t)kThreads + threadIdx.x; s < host_len; s += (int64_t)gridDim.x * kThreads) {
+    int v = host[u * host_len + s];
+    if (s < n) {
+      // audioop.mul: clamp to [-32768, 32767] then floor; audioop.add: saturate.
+      double g = (double)trig[u * trig_len + s] * factor;
+      if (g > 32767.0) g = 32767.0;
+      else if (g < -32767.0) g = -32768.0;
+      v += (int)floor(g);
+      v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
+    }
+    out[u * host_len + s] = (int16_t)v;
+  }
+}
+
+// ------------------------------------------------------------------ host side
+bool smooth235(int n) {
+  for (int f : {2, 3, 5})
+    while (n % f == 0) n /= f;
+  return n == 1;
+}
+
+std::vector<int> factorize(int M) {
+  std::vector<int> r;
+  int n = M;
+  while (n % 4 == 0) {
+    r.push_back(4);
+    n /= 4;
+  }
+  while (n % 2 == 0) {
+    r.push_back(2);
+    n /= 2;
+  }
+  while (n % 3 == 0) {
+    r.push_back(3);
+    n /= 3;
+  }
+  while (n % 5 == 0) {
+    r.push_back(5);
+    n /= 5;
+  }
+  return r;
+}
+
+double fft_cost(int M) {
+  double c = 0;
+  for (int r : factorize(M)) c += M * (1.0 + (r == 2 ? 5.0 : r == 3 ? 8.0 : r == 4 ? 8.5 : 11.2) / 8.0);
+  return c;
+}
+
+int choose_bluestein_M(int N) {
+  const int lo = 2 * N - 1;
+  int best = 0;
+  double bc = 1e300;
+  for (int m = lo; m <= 4 * lo; ++m) {
+    if (!smooth235(m)) continue;
+    const double c = fft_cost(m);
+    if (c < bc) {
+      bc = c;
+      best = m;
+    }
+  }
+  return best;
+}
+
+void host_fft(std::vector<std::complex<double>>& x) {  // forward, O(M^2) fine at plan time
+  const int M = (int)x.size();
+  std::vector<std::complex<double>> y(M), tw(M);
+  for (int k = 0; k < M; ++k) tw[k] = std::polar(1.0, -2.0 * M_PI * k / M);
+  for (int k = 0; k < M; ++k) {
+    std::complex<double> acc = 0;
+    for (int n = 0; n < M; ++n) acc += x[n] * tw[(int64_t)k * n % M];
+    y[k] = acc;
+  }
+  x.swap(y);
+}
+
+}  // namespace
+
+struct abd_mfcc_plan {
+  MfccDev dev;
+  int sr, mel_kind;
+  int64_t length;
+  void* block = nullptr;
+};
+
+extern "C" {
+
+int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels, int n_mfcc, int mel_kind,
+                         int pad_mode, float top_db, int64_t length, abd_mfcc_plan** plan) {
+  ABD_CHECK(plan != nullptr, ABD_E_INVALID, "plan out-pointer is NULL");
+  ABD_CHECK(n_fft >= 2 && hop_length >= 1 && n_mels >= 1 && n_mfcc >= 1 && n_mfcc <= n_mels, ABD_E_INVALID,
+            "bad MFCC geometry n_fft=%d hop=%d n_mels=%d n_mfcc=%d", n_fft, hop_length, n_mels, n_mfcc);
+  ABD_CHECK(n_mels <= 256, ABD_E_UNSUPPORTED, "n_mels > 256 unsupported");
+  ABD_CHECK(length > n_fft / 2, ABD_E_INVALID, "length %lld too short for reflect padding of %d",
+            (long long)length, n_fft / 2);
+  ABD_CHECK(mel_kind == ABD_MEL_HTK || mel_kind == ABD_MEL_SLANEY, ABD_E_INVALID, "bad mel kind");
+  const int N = n_fft;
+  const bool blue = !smooth235(N);
+  const int M = blue ? choose_bluestein_M(N) : N;
+  ABD_CHECK(M > 0 && M <= kMaxComplexPerBlock, ABD_E_UNSUPPORTED, "FFT length %d too large", M);
+  auto* pl = new abd_mfcc_plan();
+  MfccDev& d = pl->dev;
+  d.N = N;
+  d.hop = hop_length;
+  d.pad = N / 2;
+  d.pad_mode = pad_mode;
+  d.M = M;
+  d.bluestein = blue ? 1 : 0;
+  d.n_freqs = N / 2 + 1;
+  d.n_mels = n_mels;
+  d.n_mfcc = n_mfcc;
+  d.L = length;
+  d.T = (int)(1 + (length + 2 * (N / 2) - N) / hop_length);
+  d.top_db = top_db;
+  const int P = (d.T + 1) / 2;
+  int ppb_max = std::max(1, kMaxComplexPerBlock / M);
+  int chunks = (P + ppb_max - 1) / ppb_max;
+  d.ppb = (P + chunks - 1) / chunks;
+  d.chunks = (P + d.ppb - 1) / d.ppb;
+  auto rad = factorize(M);
+  d.n_pass = (int)rad.size();
+  int Ns = 1;
+  for (int i = 0; i < d.n_pass; ++i) {
+    d.radix[i] = rad[i];
+    d.ns[i] = Ns;
+    Ns *= rad[i];
+  }
+  pl->sr = sample_rate;
+  pl->mel_kind = mel_kind;
+  pl->length = length;
+
+  // ---- host tables (double precision, rounded once to fp32)
+  std::vector<float2> tw(M), chirp_in(N), vhat(M), chirp_out(N);
+  std::vector<float> win(N);
+  for (int k = 0; k < M; ++k) {
+    const double a = -2.0 * M_PI * k / M;
+    tw[k] = make_float2((float)cos(a), (float)sin(a));
+  }
+  std::vector<double> hann(N);
+  for (int n = 0; n < N; ++n) {
+    hann[n] = 0.5 - 0.5 * cos(2.0 * M_PI * n / N);
+    win[n] = (float)hann[n];
+  }
+  if (blue) {
+    std::vector<std::complex<double>> w(N), v(M, 0.0);
+    for (int n = 0; n < N; ++n) {
+      const int64_t q = ((int64_t)n * n) % (2 * (int64_t)N);
+      w[n] = std::polar(1.0, M_PI * (double)q / N);
+      const std::complex<double> ci = hann[n] * std::conj(w[n]);
+      chirp_in[n] = make_float2((float)ci.real(), (float)ci.imag());
+      const std::complex<double> co = w[n] / (double)M;
+      chirp_out[n] = make_float2((float)co.real(), (float)co.imag());
+    }
+    v[0] = w[0];
+    for (int m = 1; m < N; ++m) {
+      v[m] = w[m];
+      v[M - m] = w[m];
+    }
+    host_fft(v);
+    for (int m = 0; m < M; ++m) vhat[m] = make_float2((float)v[m].real(), (float)(-v[m].imag()));
+  }
+  // mel filterbank (n_freqs x n_mels), sparse per mel
+  const int nf = d.n_freqs;
+  std::vector<double> fb((size_t)nf * n_mels, 0.0);
+  if (mel_kind == ABD_MEL_HTK) {
+    // torchaudio.functional.melscale_fbanks(norm=None, mel_scale="htk"), f_max = sr // 2
+    auto h2m = [](double f) { return 2595.0 * log10(1.0 + f / 700.0); };
+    auto m2h = [](double m) { return 700.0 * (pow(10.0, m / 2595.0) - 1.0); };
+    const double fmax = (double)(sample_rate / 2);
+    std::vector<double> fpts(n_mels + 2);
+    const double m0 = h2m(0.0), m1 = h2m(fmax);
+    for (int i = 0; i < n_mels + 2; ++i) fpts[i] = m2h(m0 + (m1 - m0) * i / (n_mels + 1));
+    for (int k = 0; k < nf; ++k) {
+      const double f = fmax * k / (nf - 1);
+      for (int m = 0; m < n_mels; ++m) {
+        const double down = (f - fpts[m]) / (fpts[m + 1] - fpts[m]);
+        const double up = (fpts[m + 2] - f) / (fpts[m + 2] - fpts[m + 1]);
+        fb[(size_t)k * n_mels + m] = std::max(0.0, std::min(down, up));
+      }
+    }
+  } else {
+    // librosa.filters.mel(htk=False, norm="slaney"), stored as float32 like librosa
+    auto h2m = [](double f) {
+      const double fsp = 200.0 / 3.0, minlog = 1000.0, minmel = minlog / fsp, step = log(6.4) / 27.0;
+      return f >= minlog ? minmel + log(f / minlog) / step : f / fsp;
+    };
+    auto m2h = [](double m) {
+      const double fsp = 200.0 / 3.0, minlog = 1000.0, minmel = minlog / fsp, step = log(6.4) / 27.0;
+      return m >= minmel ? minlog * exp(step * (m - minmel)) : fsp * m;
+    };
+    const double fmax = sample_rate / 2.0;
+    std::vector<double> melf(n_mels + 2);
+    const double m0 = h2m(0.0), m1 = h2m(fmax);
+    for (int i = 0; i < n_mels + 2; ++i) melf[i] = m2h(m0 + (m1 - m0) * i / (n_mels + 1));
+    for (int m = 0; m < n_mels; ++m) {
+      const double enorm = 2.0 / (melf[m + 2] - melf[m]);
+      for (int k = 0; k < nf; ++k) {
+        const double f = (double)k * sample_rate / N;
+        const double lower = -(melf[m] - f) / (melf[m + 1] - melf[m]);
+        const double upper = (melf[m + 2] - f) / (melf[m + 2] - melf[m + 1]);
+        fb[(size_t)k * n_mels + m] = (double)(float)(std::max(0.0, std::min(lower, upper)) * enorm);
+      }
+    }
+  }
+  std::vector<int> mstart(n_mels), mcount(n_mels), moff(n_mels);
+  std::vector<float> mw;
+  for (int m = 0; m < n_mels; ++m) {
+    int lo = -1, hi = -1;
+    for (int k = 0; k < nf; ++k)
+      if (fb[(size_t)k * n_mels + m] != 0.0) {
+        if (lo < 0) lo = k;
+        hi = k;
+      }
+    moff[m] = (int)mw.size();
+    if (lo < 0) {
+      mstart[m] = 0;
+      mcount[m] = 0;
+      continue;
+    }
+    mstart[m] = lo;
+    mcount[m] = hi - lo + 1;
+    for (int k = lo; k <= hi; ++k) mw.push_back((float)fb[(size_t)k * n_mels + m]);
+  }
+  if (mw.empty()) mw.push_back(0.0f);
+  std::vector<float> dct((size_t)n_mels * n_mfcc);
+  for (int m = 0; m < n_mels; ++m)
+    for (int c = 0; c < n_mfcc; ++c) {
+      double v = cos(M_PI / n_mels * (m + 0.5) * c) * sqrt(2.0 / n_mels);
+      if (c == 0) v *= 1.0 / sqrt(2.0);
+      dct[(size_t)m * n_mfcc + c] = (float)v;
+    }
+
+  // ---- one device block for every table
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  size_t off_tw = 0, sz = al(M * sizeof(float2));
+  size_t off_ci = sz;
+  sz += al(N * sizeof(float2));
+  size_t off_vh = sz;
+  sz += al(M * sizeof(float2));
+  size_t off_co = sz;
+  sz += al(N * sizeof(float2));
+  size_t off_win = sz;
+  sz += al(N * sizeof(float));
+  size_t off_ms = sz;
+  sz += al(n_mels * sizeof(int));
+  size_t off_mc = sz;
+  sz += al(n_mels * sizeof(int));
+  size_t off_mo = sz;
+  sz += al(n_mels * sizeof(int));
+  size_t off_mw = sz;
+  sz += al(mw.size() * sizeof(float));
+  size_t off_dct = sz;
+  sz += al(dct.size() * sizeof(float));
+  std::vector<char> host(sz, 0);
+  memcpy(&host[off_tw], tw.data(), M * sizeof(float2));
+  memcpy(&host[off_ci], chirp_in.data(), N * sizeof(float2));
+  memcpy(&host[off_vh], vhat.data(), M * sizeof(float2));
+  memcpy(&host[off_co], chirp_out.data(), N * sizeof(float2));
+  memcpy(&host[off_win], win.data(), N * sizeof(float));
+  memcpy(&host[off_ms], mstart.data(), n_mels * sizeof(int));
+  memcpy(&host[off_mc], mcount.data(), n_mels * sizeof(int));
+  memcpy(&host[off_mo], moff.data(), n_mels * sizeof(int));
+  memcpy(&host[off_mw], mw.data(), mw.size() * sizeof(float));
+  memcpy(&host[off_dct], dct.data(), dct.size() * sizeof(float));
+  hipError_t e = hipMalloc(&pl->block, sz);
+  if (e != hipSuccess) {
+    delete pl;
+    abd::set_last_error("hipMalloc(%zu) for MFCC tables: %s", sz, hipGetErrorString(e));
+    return (int)e;
+  }
+  e = hipMemcpy(pl->block, host.data(), sz, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(pl->block);
+    delete pl;
+    abd::set_last_error("hipMemcpy MFCC tables: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  char* b = static_cast<char*>(pl->block);
+  d.tw = reinterpret_cast<const float2*>(b + off_tw);
+  d.chirp_in = reinterpret_cast<const float2*>(b + off_ci);
+  d.vhat = reinterpret_cast<const float2*>(b + off_vh);
+  d.chirp_out = reinterpret_cast<const float2*>(b + off_co);
+  d.window = reinterpret_cast<const float*>(b + off_win);
+  d.mel_start = reinterpret_cast<const int*>(b + off_ms);
+  d.mel_count = reinterpret_cast<const int*>(b + off_mc);
+  d.mel_off = reinterpret_cast<const int*>(b + off_mo);
+  d.mel_w = reinterpret_cast<const float*>(b + off_mw);
+  d.dct = reinterpret_cast<const float*>(b + off_dct);
+  *plan = pl;
+  return ABD_OK;
+}
+
+void abd_mfcc_plan_destroy(abd_mfcc_plan* plan) {
+  if (!plan) return;
+  if (plan->block) (void)hipFree(plan->block);
+  delete plan;
+}
+
+int abd_mfcc_plan_frames(const abd_mfcc_plan* plan) { return plan ? plan->dev.T : -1; }
+
+int abd_mfcc_plan_describe(const abd_mfcc_plan* plan, int* fft_size, int* bluestein, int* n_passes, int* radices) {
+  ABD_CHECK(plan != nullptr, ABD_E_INVALID, "NULL plan");
+  if (fft_size) *fft_size = plan->dev.M;
+  if (bluestein) *bluestein = plan->dev.bluestein;
+  if (n_passes) *n_passes = plan->dev.n_pass;
+  if (radices)
+    for (int i = 0; i < plan->dev.n_pass; ++i) radices[i] = plan->dev.radix[i];
+  return ABD_OK;
+}
+
+size_t abd_mfcc_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch) {
+  if (!plan) return 0;
+  const MfccDev& d = plan->dev;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return al((size_t)batch * d.T * d.n_mels * sizeof(float)) + al((size_t)batch * d.chunks * sizeof(float)) +
+         al((size_t)batch * sizeof(float));
+}
+
+static InjDev make_inj(const abd_inject* inj) {
+  InjDev r{};
+  if (!inj) {
+    r.mode = ABD_INJECT_NONE;
+    return r;
+  }
+  r.mode = inj->mode;
+  r.trig = inj->trigger;
+  r.trig_len = inj->trigger_len;
+  r.poison = inj->poison;
+  r.position = inj->position;
+  r.snr_db = inj->snr_db;
+  r.patch = inj->patch;
+  r.pt0 = inj->patch_t0;
+  r.pt1 = inj->patch_t1;
+  r.pc0 = inj->patch_c0;
+  r.pc1 = inj->patch_c1;
+  r.pval = inj->patch_value;
+  if (r.mode == ABD_INJECT_NONE && r.patch) r.mode = -1;  // patch-only: rows still selected by poison
+  return r;
+}
+
+static int check_inj(const InjDev& r) {
+  if (r.mode > 0) {
+    ABD_CHECK(r.trig != nullptr && r.trig_len > 0, ABD_E_INVALID, "injection mode %d needs a trigger", r.mode);
+    if (r.mode >= ABD_INJECT_SNR_WINDOW)
+      ABD_CHECK(r.position != nullptr, ABD_E_INVALID, "windowed injection needs per-row positions");
+  }
+  return ABD_OK;
+}
+
+int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride, const int32_t* rows,
+                 int64_t batch, const abd_inject* inj, float* out, void* workspace, size_t workspace_bytes,
+                 abd_stream_t stream) {
+  ABD_CHECK(batch >= 0, ABD_E_INVALID, "negative batch");
+  if (batch == 0) return ABD_OK;
+  ABD_CHECK(plan && wave && out, ABD_E_INVALID, "NULL argument");
+  ABD_CHECK(row_stride >= plan->length, ABD_E_INVALID, "row_stride < length");
+  ABD_CHECK(workspace && workspace_bytes >= abd_mfcc_workspace_bytes(plan, batch), ABD_E_WORKSPACE,
+            "workspace too small (%zu < %zu)", workspace_bytes, abd_mfcc_workspace_bytes(plan, batch));
+  const MfccDev& d = plan->dev;
+  InjDev ij = make_inj(inj);
+  int rc = check_inj(ij);
+  if (rc) return rc;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* ws = static_cast<char*>(workspace);
+  float* ws_db = reinterpret_cast<float*>(ws);
+  float* ws_max = reinterpret_cast<float*>(ws + al((size_t)batch * d.T * d.n_mels * sizeof(float)));
+  float* ws_scale = reinterpret_cast<float*>(ws + al((size_t)batch * d.T * d.n_mels * sizeof(float)) +
+                                             al((size_t)batch * d.chunks * sizeof(float)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const float* rowscale = nullptr;
+  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY) {
+    row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
+    ABD_LAUNCH_CHECK();
+    rowscale = ws_scale;
+  }
+  const int64_t nblk = batch * d.chunks;
+  ABD_CHECK(nblk < (1LL << 31), ABD_E_INVALID, "batch too large");
+  const size_t lds = 2 * (size_t)d.ppb * d.M * sizeof(float2);
+  abd::prof_begin(abd::PH_STFT_MEL, s);
+  stft_mel_kernel<<<dim3((unsigned)nblk), dim3(kThreads), lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale,
+                                                                  ws_db, ws_max);
+  abd::prof_end(abd::PH_STFT_MEL, s);
+  ABD_LAUNCH_CHECK();
+  abd::prof_begin(abd::PH_DB_DCT, s);
+  db_dct_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT - 1) / kTT)), dim3(kThreads), 0, s>>>(d, ws_db, ws_max,
+                                                                                                   ij, out);
+  abd::prof_end(abd::PH_DB_DCT, s);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+size_t abd_inject_workspace_bytes(int64_t batch) { return ((size_t)batch * sizeof(float) + 255) & ~(size_t)255; }
+
+int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t length, const int32_t* rows, int64_t batch,
+                            const abd_inject* inj, float* out, void* workspace, size_t workspace_bytes,
+                            abd_stream_t stream) {
+  if (batch == 0) return ABD_OK;
+  ABD_CHECK(wave && out, ABD_E_INVALID, "NULL argument");
+  InjDev ij = make_inj(inj);
+  int rc = check_inj(ij);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const float* rowscale = nullptr;
+  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY) {
+    ABD_CHECK(workspace && workspace_bytes >= abd_inject_workspace_bytes(batch), ABD_E_WORKSPACE,
+              "workspace too small");
+    row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
+                                                                      static_cast<float*>(workspace));
+    ABD_LAUNCH_CHECK();
+    rowscale = static_cast<const float*>(workspace);
+  }
+  const unsigned gx = (unsigned)std::min<int64_t>((length + kThreads - 1) / kThreads, 64);
+  inject_wave_kernel<<<dim3(gx, (unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
+                                                                         rowscale, out);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+int abd_pydub_overlay_i16(const int16_t* host, int64_t host_len, const int16_t* trig, int64_t trig_len,
+                          const float* gain_db, int64_t batch, int16_t* out, abd_stream_t stream) {
+  ABD_CHECK(host && trig && gain_db && out, ABD_E_INVALID, "NULL argument");
+  if (batch == 0) return ABD_OK;
+  const unsigned gx = (unsigned)std::min<int64_t>((host_len + kThreads - 1) / kThreads, 64);
+  pydub_overlay_kernel<<<dim3(gx, (unsigned)batch), dim3(kThreads), 0, static_cast<hipStream_t>(stream)>>>(
+      host, host_len, trig, trig_len, gain_db, out);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+}  // extern "C"

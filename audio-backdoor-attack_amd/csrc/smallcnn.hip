@@ -1,0 +1,1586 @@
+// smallcnn training/eval step for gfx950: forward, backward, loss, Adam, metrics.
+//
+// Replaces utils/models.py:17-65 (smallcnn), utils/training_tools.py:52-85 (train
+// inner step: CrossEntropyLoss on log-probs, backward, optim.Adam.step, loss/acc/ASR
+// bookkeeping) and :87-134 (test).
+//
+// Layout (DESIGN.md "smallcnn"): activations are NHWC (channels innermost) so every
+// implicit-GEMM operand row is a contiguous 128/256-byte channel vector; the flatten
+// before fc1 is written in the reference's NCHW (c,h,w) order so fc1.weight is used
+// exactly as torch stores it.  The 2x2 convolutions, their data/weight gradients and
+// fc1 run as fp32-in/fp32-accumulate MFMA (v_mfma_f32_32x32x2_f32: exact f32 FMA
+// chains, the only MFMA that meets the 1e-4 fp32 parity target).  conv1 (K=4) is
+// VALU work and is recomputed in every pass instead of materialising its
+// (B,64,H0-1,W0-1) output.  BatchNorm uses batch statistics reduced through
+// per-block partials summed in double (deterministic order), max-pool argmax is
+// recomputed (first maximum in scan order, like ATen's CPU kernel), and dropout masks
+// come from a counter-based hash (or are supplied, for parity tests).
+#include "abd_common.h"
+#include "prof.h"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int kT = 256;
+using abd::kWave;
+constexpr float kEps = 1e-5f;
+constexpr float kMomentum = 0.1f;
+constexpr float kP1 = 0.4f, kP2 = 0.5f;
+constexpr int kR1 = 4;  // conv1 rows per block
+
+struct Geo {
+  int H0, W0, K, H1, W1, W1p, H2, W2, H2p, W2p, H3, W3, H3p, W3p, flat;
+};
+
+Geo make_geo(int H0, int W0, int K) {
+  Geo g;
+  g.H0 = H0;
+  g.W0 = W0;
+  g.K = K;
+  g.H1 = H0 - 1;
+  g.W1 = W0 - 1;
+  g.W1p = g.W1 / 3;
+  g.H2 = g.H1 - 1;
+  g.W2 = g.W1p - 1;
+  g.H2p = g.H2 / 2 + 1;
+  g.W2p = g.W2 / 2 + 1;
+  g.H3 = g.H2p - 1;
+  g.W3 = g.W2p - 1;
+  g.H3p = (g.H3 - 2) / 2 + 1;
+  g.W3p = g.W3 / 2 + 1;
+  g.flat = 32 * g.H3p * g.W3p;
+  return g;
+}
+
+// ------------------------------------------------------------------ parameter layout
+enum {
+  P_C1W, P_C1B, P_BN1W, P_BN1B, P_C2W, P_C2B, P_BN2W, P_BN2B,
+  P_C3W, P_C3B, P_BN3W, P_BN3B, P_F1W, P_F1B, P_F2W, P_F2B, P_COUNT
+};
+
+void param_sizes(const Geo& g, int64_t* sz) {
+  const int64_t s[P_COUNT] = {256, 64, 64, 64, 16384, 64, 64, 64, 8192, 32, 32, 32,
+                              128LL * g.flat, 128, (int64_t)g.K * 128, g.K};
+  for (int i = 0; i < P_COUNT; ++i) sz[i] = s[i];
+}
+
+// ------------------------------------------------------------------ dropout hash
+__device__ __forceinline__ bool keep_hash(uint64_t seed, uint64_t stream, uint64_t idx, float p) {
+  uint64_t z = seed ^ (stream * 0x9E3779B97F4A7C15ull) ^ (idx * 0xD1B54A32D192ED03ull);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+  return u >= p;  // keep with probability 1-p (torch: bernoulli_(1-p))
+}
+
+struct DropArgs {
+  const uint8_t* mask_in;
+  uint8_t* mask_out;
+  uint64_t seed, stream;
+  float p, scale;
+  int enabled;
+};
+
+__device__ __forceinline__ float drop_apply(const DropArgs& d, int64_t idx, float v) {
+  if (!d.enabled) return v;
+  bool k = d.mask_in ? (d.mask_in[idx] != 0) : keep_hash(d.seed, d.stream, (uint64_t)idx, d.p);
+  if (d.mask_out) d.mask_out[idx] = k ? 1 : 0;
+  return v * (k ? d.scale : 0.0f);
+}
+
+// ------------------------------------------------------------------ block helpers
+// Reduce `nvals` per-thread values over the threads sharing a channel (channel = tid % C)
+// and write them as partials part[(j*C + c)*nblk + blk].
+template <int NV>
+__device__ __forceinline__ void channel_partials(float (&v)[NV], int C, float* part, int nblk, int blk) {
+  __shared__ float red[NV * kT];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) red[j * kT + t] = v[j];
+  __syncthreads();
+  if (t < C) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float s = 0.0f;
+      for (int q = t; q < kT; q += C) s += red[j * kT + q];
+      part[((int64_t)j * C + t) * nblk + blk] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ conv1 (VALU, recomputed)
+struct C1Args {
+  const float* x;   // (B, H0, W0)
+  const float* w;   // conv1.weight (64,1,2,2)
+  const float* b;   // conv1.bias
+  const float4* coef;  // BN1 (mean, invstd, alpha, beta')
+  const float* dp1;    // (B,H1,W1p,64) grad of pool1 output
+  const float4* bcoef; // BN1 backward (g, mdy, mdyx, -)
+  float* p1;
+  float* part;
+  int nblk;
+  Geo g;
+  int B;
+};
+
+// Stage x rows [h0, h0+kR1] of utterance b into LDS.
+__device__ __forceinline__ void stage_x(const C1Args& a, int b, int h0, float* xs) {
+  const int rows = min(kR1 + 1, a.g.H0 - h0);
+  const float* src = a.x + ((int64_t)b * a.g.H0 + h0) * a.g.W0;
+  for (int i = threadIdx.x; i < rows * a.g.W0; i += kT) xs[i] = src[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ float conv1_at(const float* xs, int W0, int hl, int w, float w00, float w01, float w10,
+                                          float w11, float bias) {
+  const float* r0 = xs + hl * W0 + w;
+  const float* r1 = r0 + W0;
+  float v = bias;
+  v = fmaf(w00, r0[0], v);
+  v = fmaf(w01, r0[1], v);
+  v = fmaf(w10, r1[0], v);
+  v = fmaf(w11, r1[1], v);
+  return fmaxf(v, 0.0f);
+}
+
+// forward stats: sum / sumsq of relu(conv1) per channel
+__global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
+  __shared__ float xs[(kR1 + 1) * 128];
+  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
+  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
+  stage_x(a, b, h0, xs);
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
+  const int rows = min(kR1, a.g.H1 - h0);
+  float v[2] = {0.0f, 0.0f};
+  for (int p = sub; p < rows * a.g.W1; p += 4) {
+    const int hl = p / a.g.W1, w = p - hl * a.g.W1;
+    const float r = conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb);
+    v[0] += r;
+    v[1] = fmaf(r, r, v[1]);
+  }
+  channel_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
+}
+
+__device__ __forceinline__ int argmax3(float y0, float y1, float y2, float& best) {
+  int j = 0;
+  best = y0;
+  if (y1 > best) {
+    best = y1;
+    j = 1;
+  }
+  if (y2 > best) {
+    best = y2;
+    j = 2;
+  }
+  return j;
+}
+
+// forward: relu(conv1) -> BN1 -> maxpool(1,3) -> p1 (NHWC)
+__global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
+  __shared__ float xs[(kR1 + 1) * 128];
+  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
+  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
+  stage_x(a, b, h0, xs);
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
+  const float4 cf = a.coef[c];
+  const int rows = min(kR1, a.g.H1 - h0);
+  for (int p = sub; p < rows * a.g.W1p; p += 4) {
+    const int hl = p / a.g.W1p, wo = p - hl * a.g.W1p;
+    const int w = 3 * wo;
+    const float y0 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb), cf.w);
+    const float y1 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w + 1, w00, w01, w10, w11, bb), cf.w);
+    const float y2 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w + 2, w00, w01, w10, w11, bb), cf.w);
+    float best;
+    argmax3(y0, y1, y2, best);
+    a.p1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c] = best;
+  }
+}
+
+// backward stats: s1 = sum dy, s2 = sum dy * xhat over pool1 argmax positions
+__global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
+  __shared__ float xs[(kR1 + 1) * 128];
+  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
+  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
+  stage_x(a, b, h0, xs);
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
+  const float4 cf = a.coef[c];
+  const int rows = min(kR1, a.g.H1 - h0);
+  float v[2] = {0.0f, 0.0f};
+  for (int p = sub; p < rows * a.g.W1p; p += 4) {
+    const int hl = p / a.g.W1p, wo = p - hl * a.g.W1p;
+    const int w = 3 * wo;
+    const float r0 = conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb);
+    const float r1 = conv1_at(xs, a.g.W0, hl, w + 1, w00, w01, w10, w11, bb);
+    const float r2 = conv1_at(xs, a.g.W0, hl, w + 2, w00, w01, w10, w11, bb);
+    float best;
+    const int j = argmax3(fmaf(cf.z, r0, cf.w), fmaf(cf.z, r1, cf.w), fmaf(cf.z, r2, cf.w), best);
+    const float rs = j == 0 ? r0 : (j == 1 ? r1 : r2);
+    const float dy = a.dp1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c];
+    v[0] += dy;
+    v[1] = fmaf(dy, (rs - cf.x) * cf.y, v[1]);
+  }
+  channel_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
+}
+
+// backward: BN1 dx -> relu mask -> conv1 weight / bias gradient partials (5 per channel)
+__global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
+  __shared__ float xs[(kR1 + 1) * 128];
+  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
+  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
+  stage_x(a, b, h0, xs);
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
+  const float4 cf = a.coef[c];
+  const float4 bc = a.bcoef[c];  // (g = gamma*invstd, mdy, mdyx, -)
+  const int rows = min(kR1, a.g.H1 - h0);
+  const int nwin = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
+  float v[5] = {0, 0, 0, 0, 0};
+  for (int p = sub; p < rows * nwin; p += 4) {
+    const int hl = p / nwin, wo = p - hl * nwin;
+    const int w = 3 * wo;
+    const int nw = min(3, a.g.W1 - w);
+    float r[3], y[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      r[j] = (j < nw) ? conv1_at(xs, a.g.W0, hl, w + j, w00, w01, w10, w11, bb) : 0.0f;
+      y[j] = fmaf(cf.z, r[j], cf.w);
+    }
+    int jm = -1;
+    float dyv = 0.0f;
+    if (wo < a.g.W1p) {
+      float best;
+      jm = argmax3(y[0], y[1], y[2], best);
+      dyv = a.dp1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= nw) continue;
+      const float dy = (j == jm) ? dyv : 0.0f;
+      const float xh = (r[j] - cf.x) * cf.y;
+      const float dx = (dy - bc.y - xh * bc.z) * bc.x;
+      const float dz = r[j] > 0.0f ? dx : 0.0f;
+      const float* x0 = xs + hl * a.g.W0 + w + j;
+      v[0] = fmaf(dz, x0[0], v[0]);
+      v[1] = fmaf(dz, x0[1], v[1]);
+      v[2] = fmaf(dz, x0[a.g.W0], v[2]);
+      v[3] = fmaf(dz, x0[a.g.W0 + 1], v[3]);
+      v[4] += dz;
+    }
+  }
+  channel_partials<5>(v, 64, a.part, a.nblk, blockIdx.x);
+}
+
+// ------------------------------------------------------------------ BN statistics
+// part layout: [(j*C + c) * nblk + blk], j = 0 sum, 1 sumsq
+__global__ void __launch_bounds__(kT) bn_finalize_kernel(const float* part, int nblk, int C, double count,
+                                                         const float* gamma, const float* beta, float* rm, float* rv,
+                                                         float4* coef) {
+  const int c = blockIdx.x;
+  double s = 0.0, ss = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kT) {
+    s += part[(int64_t)c * nblk + i];
+    ss += part[((int64_t)C + c) * nblk + i];
+  }
+  __shared__ double red[2][kT / kWave];
+  s = abd::wave_sum_d(s);
+  ss = abd::wave_sum_d(ss);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = ss;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    ss = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    const double mean = s / count;
+    double var = ss / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)kEps));
+    const float alpha = gamma[c] * invstd;
+    const float meanf = (float)mean;
+    coef[c] = make_float4(meanf, invstd, alpha, beta[c] - meanf * alpha);
+    if (rm) {
+      const double mo = (double)kMomentum;
+      rm[c] = (float)(mo * mean + (1.0 - mo) * (double)rm[c]);
+      rv[c] = (float)(mo * (var * count / (count - 1.0)) + (1.0 - mo) * (double)rv[c]);
+    }
+  }
+}
+
+__global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, int C,
+                                    float4* coef) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.0f / sqrtf(rv[c] + kEps);
+  const float alpha = gamma[c] * invstd;
+  coef[c] = make_float4(rm[c], invstd, alpha, beta[c] - rm[c] * alpha);
+}
+
+// backward finalize: s1 = sum dy (-> dbeta), s2 = sum dy*xhat (-> dgamma); coefficients for dx
+__global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, int nblk, int C, double count,
+                                                             const float* gamma, const float4* coef, float* dgamma,
+                                                             float* dbeta, float4* bcoef) {
+  const int c = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kT) {
+    s1 += part[(int64_t)c * nblk + i];
+    s2 += part[((int64_t)C + c) * nblk + i];
+  }
+  __shared__ double red[2][kT / kWave];
+  s1 = abd::wave_sum_d(s1);
+  s2 = abd::wave_sum_d(s2);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s1;
+    red[1][threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s1 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    dgamma[c] = (float)s2;
+    dbeta[c] = (float)s1;
+    bcoef[c] = make_float4(gamma[c] * coef[c].y, (float)(s1 / count), (float)(s2 / count), 0.0f);
+  }
+}
+
+// sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
+__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out) {
+  const int col = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kT) s += part[(int64_t)col * nblk + i];
+  __shared__ double red[kT / kWave];
+  s = abd::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[col] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------ BN + max-pool (layers 2, 3)
+struct PoolArgs {
+  const float* r;  // NHWC (B,H,W,C) relu(conv) output
+  int B, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw;
+  const float4* coef;
+  float* out;      // NHWC pooled, or NCHW-flat (flat_n > 0)
+  int flat_n;
+  DropArgs drop;
+  const float* dp;     // grad wrt pooled output (same layout as out)
+  const float4* bcoef;
+  float* dz;           // NHWC
+  float* part;
+  int nblk;
+};
+
+__device__ __forceinline__ int pool_argmax(const PoolArgs& a, int b, int ho, int wo, int c, float4 cf, float& best) {
+  best = -INFINITY;
+  int arg = -1;
+  for (int i = 0; i < a.kh; ++i) {
+    const int h = ho * a.sh - a.ph + i;
+    if (h < 0 || h >= a.H) continue;
+    for (int j = 0; j < a.kw; ++j) {
+      const int w = wo * a.sw - a.pw + j;
+      if (w < 0 || w >= a.W) continue;
+      const float y = fmaf(cf.z, a.r[(((int64_t)b * a.H + h) * a.W + w) * a.C + c], cf.w);
+      if (y > best) {
+        best = y;
+        arg = h * a.W + w;
+      }
+    }
+  }
+  return arg;
+}
+
+__device__ __forceinline__ int64_t pooled_index(const PoolArgs& a, int b, int ho, int wo, int c) {
+  if (a.flat_n > 0) return (int64_t)b * a.flat_n + ((int64_t)c * a.Ho + ho) * a.Wo + wo;
+  return (((int64_t)b * a.Ho + ho) * a.Wo + wo) * a.C + c;
+}
+
+__global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
+  const int64_t total = (int64_t)a.B * a.Ho * a.Wo * a.C;
+  for (int64_t o = blockIdx.x * (int64_t)kT + threadIdx.x; o < total; o += (int64_t)gridDim.x * kT) {
+    const int c = (int)(o % a.C);
+    int64_t q = o / a.C;
+    const int wo = (int)(q % a.Wo);
+    q /= a.Wo;
+    const int ho = (int)(q % a.Ho);
+    const int b = (int)(q / a.Ho);
+    float best;
+    pool_argmax(a, b, ho, wo, c, a.coef[c], best);
+    const int64_t oi = pooled_index(a, b, ho, wo, c);
+    a.out[oi] = drop_apply(a.drop, oi, best);
+  }
+}
+
+__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) {
+  const int64_t total = (int64_t)a.B * a.Ho * a.Wo * a.C;
+  const int c = threadIdx.x % a.C;  // fixed per thread: grid stride is a multiple of C
+  const float4 cf = a.coef[c];
+  float v[2] = {0.0f, 0.0f};
+  for (int64_t o = blockIdx.x * (int64_t)kT + threadIdx.x; o < total; o += (int64_t)gridDim.x * kT) {
+    int64_t q = o / a.C;
+    const int wo = (int)(q % a.Wo);
+    q /= a.Wo;
+    const int ho = (int)(q % a.Ho);
+    const int b = (int)(q / a.Ho);
+    float best;
+    const int arg = pool_argmax(a, b, ho, wo, c, cf, best);
+    const float dy = a.dp[pooled_index(a, b, ho, wo, c)];
+    const float rv = a.r[(((int64_t)b * a.H) * a.W + arg) * a.C + c];
+    v[0] += dy;
+    v[1] = fmaf(dy, (rv - cf.x) * cf.y, v[1]);
+  }
+  channel_partials<2>(v, a.C, a.part, a.nblk, blockIdx.x);
+}
+
+// dz = relu'(r) * BN backward(dy scattered to the argmax); bias-grad partials
+__global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a) {
+  const int64_t total = (int64_t)a.B * a.H * a.W * a.C;
+  const int c = threadIdx.x % a.C;
+  const float4 cf = a.coef[c];
+  const float4 bc = a.bcoef[c];
+  float v[1] = {0.0f};
+  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    int64_t q = e / a.C;
+    const int w = (int)(q % a.W);
+    q /= a.W;
+    const int h = (int)(q % a.H);
+    const int b = (int)(q / a.H);
+    const int ho = (h + a.ph) / a.sh, wo = (w + a.pw) / a.sw;
+    float dy = 0.0f;
+    if (ho < a.Ho && wo < a.Wo) {
+      float best;
+      const int arg = pool_argmax(a, b, ho, wo, c, cf, best);
+      if (arg == h * a.W + w) dy = a.dp[pooled_index(a, b, ho, wo, c)];
+    }
+    const float rv = a.r[e];
+    const float xh = (rv - cf.x) * cf.y;
+    const float dx = (dy - bc.y - xh * bc.z) * bc.x;
+    const float dz = rv > 0.0f ? dx : 0.0f;
+    a.dz[e] = dz;
+    v[0] += dz;
+  }
+  channel_partials<1>(v, a.C, a.part, a.nblk, blockIdx.x);
+}
+
+// ------------------------------------------------------------------ fp32 MFMA GEMMs
+// NT: C[m][n] = sum_t sum_c A_t(m)[c] * Bw[n][t*Cs + c]; A_t(m) is the NHWC channel row
+// of src at output position m shifted by tap t (zero outside the source grid).
+enum { EPI_STORE = 0, EPI_CONV = 1, EPI_FC1 = 2, EPI_DROPGRAD = 3 };
+
+struct NTArgs {
+  const float* src;
+  int Hs, Ws, Cs;
+  int Ho, Wo, M;
+  int taps;
+  int dh[4], dw[4];
+  const float* Bw;
+  int ldb, N;
+  const float* bias;
+  float* out;
+  int ldc;
+  float* part;   // EPI_CONV stats partials [(j*N + n)*nblk + blk]
+  int nblk;
+  DropArgs drop;  // EPI_FC1 (dropout2 on relu(fc1)), EPI_DROPGRAD (dropout1 mask)
+};
+
+constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
+
+template <int NB, int EPI>
+__global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
+  __shared__ float As[kBM * kLDA];
+  __shared__ float Bs[NB * kLDA];
+  constexpr int NJ = NB / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * kBM;
+  const int n0 = blockIdx.y * NB;
+  const int q4 = tid & 7;
+  int rb[4], rh[4], rw[4];
+  bool rok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    rok[i] = m < a.M;
+    const int mm = rok[i] ? m : 0;
+    rb[i] = mm / (a.Ho * a.Wo);
+    const int rem = mm - rb[i] * a.Ho * a.Wo;
+    rh[i] = rem / a.Wo;
+    rw[i] = rem - rh[i] * a.Wo;
+  }
+  const int cpt = a.Cs / kKC;
+  const int nch = a.taps * cpt;
+  float4 ra[4], rbv[NJ];
+  auto load = [&](int ch) {
+    const int t = ch / cpt;
+    const int c0 = (ch - t * cpt) * kKC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hs = rh[i] + a.dh[t], ws = rw[i] + a.dw[t];
+      const bool ok = rok[i] && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws;
+      ra[i] = ok ? *reinterpret_cast<const float4*>(a.src + (((int64_t)rb[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c0 +
+                                                    4 * q4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int idx = tid + kT * j;
+      const int n = idx >> 3, q = idx & 7;
+      rbv[j] = (n0 + n < a.N) ? *reinterpret_cast<const float4*>(a.Bw + (int64_t)(n0 + n) * a.ldb + t * a.Cs + c0 + 4 * q)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x16 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* d = As + ((tid >> 3) + 32 * i) * kLDA + 4 * q4;
+      d[0] = ra[i].x;
+      d[1] = ra[i].y;
+      d[2] = ra[i].z;
+      d[3] = ra[i].w;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int idx = tid + kT * j;
+      float* d = Bs + (idx >> 3) * kLDA + 4 * (idx & 7);
+      d[0] = rbv[j].x;
+      d[1] = rbv[j].y;
+      d[2] = rbv[j].z;
+      d[3] = rbv[j].w;
+    }
+    __syncthreads();
+    if (ch + 1 < nch) load(ch + 1);
+    const float* ap = As + (wave * 32 + (lane & 31)) * kLDA + (lane >> 5);
+    const float* bp = Bs + (lane & 31) * kLDA + (lane >> 5);
+#pragma unroll
+    for (int kk = 0; kk < kKC; kk += 2) {
+      const float av = ap[kk];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bp[j * 32 * kLDA + kk], acc[j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[j][r] -> row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31 of tile j
+  float st[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    st[j][0] = 0.0f;
+    st[j][1] = 0.0f;
+    const int col = n0 + j * 32 + (lane & 31);
+    const bool cok = col < a.N;
+    float bias = 0.0f;
+    if constexpr (EPI == EPI_CONV || EPI == EPI_FC1) bias = cok ? a.bias[col] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= a.M || !cok) continue;
+      float v = acc[j][r];
+      const int64_t oi = (int64_t)m * a.ldc + col;
+      if constexpr (EPI == EPI_CONV) {
+        v = fmaxf(v + bias, 0.0f);
+        st[j][0] += v;
+        st[j][1] = fmaf(v, v, st[j][1]);
+      } else if constexpr (EPI == EPI_FC1) {
+        v = drop_apply(a.drop, oi, fmaxf(v + bias, 0.0f));
+      } else if constexpr (EPI == EPI_DROPGRAD) {
+        const bool k = a.drop.mask_in[oi] != 0;
+        v = v * (k ? a.drop.scale : 0.0f);
+      }
+      a.out[oi] = v;
+    }
+  }
+  if constexpr (EPI == EPI_CONV) {
+    if (a.part == nullptr) return;
+    // reduce over lane halves, then waves (through LDS)
+    float* red = As;  // reuse: [4 waves][NB][2]
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+      float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+      if (lane < 32) {
+        red[(wave * NB + j * 32 + lane) * 2 + 0] = s0;
+        red[(wave * NB + j * 32 + lane) * 2 + 1] = s1;
+      }
+    }
+    __syncthreads();
+    if (tid < NB && n0 + tid < a.N) {
+      float s0 = 0.0f, s1 = 0.0f;
+      for (int w = 0; w < 4; ++w) {
+        s0 += red[(w * NB + tid) * 2 + 0];
+        s1 += red[(w * NB + tid) * 2 + 1];
+      }
+      a.part[((int64_t)0 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s0;
+      a.part[((int64_t)1 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s1;
+    }
+  }
+}
+
+// TN (weight gradient): slab[blk][n][k] = sum_{m in chunk} D[m][n] * S_t(m)[c], k = t*Cs + c
+struct TNArgs {
+  const float* D;
+  int ldd;
+  const float* src;
+  int Hs, Ws, Cs;
+  int Ho, Wo, M;
+  int taps;
+  int dh[4], dw[4];
+  int N, Ktot;
+  int mchunk;
+  float* slab;
+};
+
+template <int NB, int KT>
+__global__ void __launch_bounds__(kT) gemm_tn_kernel(TNArgs a) {
+  constexpr int MR = 32;
+  __shared__ __attribute__((aligned(16))) float Ds[MR * NB];
+  __shared__ __attribute__((aligned(16))) float Ss[MR * KT];
+  constexpr int KTILES = KT / 32;
+  constexpr int TPW = (NB / 32) * KTILES / 4;  // accumulator tiles per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mstart = blockIdx.x * a.mchunk;
+  const int mend = min(a.M, mstart + a.mchunk);
+  const int k0 = blockIdx.y * KT;
+  const int n0 = blockIdx.z * NB;
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  const int tile0 = wave * TPW;
+  const int ntile = tile0 / KTILES;  // all of a wave's tiles share one n-tile
+  for (int mm = mstart; mm < mend; mm += MR) {
+    for (int idx = tid; idx < MR * NB / 4; idx += kT) {
+      const int r = idx / (NB / 4), q = idx - r * (NB / 4);
+      const int m = mm + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend) v = *reinterpret_cast<const float4*>(a.D + (int64_t)m * a.ldd + n0 + 4 * q);
+      *reinterpret_cast<float4*>(Ds + r * NB + 4 * q) = v;
+    }
+    for (int idx = tid; idx < MR * KT / 4; idx += kT) {
+      const int r = idx / (KT / 4), q = idx - r * (KT / 4);
+      const int m = mm + r;
+      const int kx = k0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend && kx < a.Ktot) {
+        const int t = kx / a.Cs, c = kx - t * a.Cs;
+        const int b = m / (a.Ho * a.Wo);
+        const int rem = m - b * a.Ho * a.Wo;
+        const int h = rem / a.Wo + a.dh[t], w = rem % a.Wo + a.dw[t];
+        if (h >= 0 && h < a.Hs && w >= 0 && w < a.Ws)
+          v = *reinterpret_cast<const float4*>(a.src + (((int64_t)b * a.Hs + h) * a.Ws + w) * a.Cs + c);
+      }
+      *reinterpret_cast<float4*>(Ss + r * KT + 4 * q) = v;
+    }
+    __syncthreads();
+    const float* ap = Ds + (lane >> 5) * NB + ntile * 32 + (lane & 31);
+#pragma unroll
+    for (int kk = 0; kk < MR; kk += 2) {
+      const float av = ap[kk * NB];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int kt = (tile0 + i) % KTILES;
+        const float bv = Ss[(kk + (lane >> 5)) * KT + kt * 32 + (lane & 31)];
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = a.slab + (int64_t)blockIdx.x * a.N * a.Ktot;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int kt = (tile0 + i) % KTILES;
+    const int k = k0 + kt * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (n < a.N && k < a.Ktot) slab[(int64_t)n * a.Ktot + k] = acc[i][r];
+    }
+  }
+}
+
+// sum slabs in order; conv layout maps (n=co, k=t*Cin+ci) -> torch (co, ci, kh, kw)
+__global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int nslab, int N, int Ktot, int conv_cin,
+                                                         float* out) {
+  const int64_t total = (int64_t)N * Ktot;
+  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    float s = 0.0f;
+    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * total + e];
+    const int n = (int)(e / Ktot), k = (int)(e % Ktot);
+    if (conv_cin > 0) {
+      const int t = k / conv_cin, ci = k % conv_cin;
+      out[((int64_t)n * conv_cin + ci) * 4 + t] = s;
+    } else {
+      out[e] = s;
+    }
+  }
+}
+
+// weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets)
+__global__ void __launch_bounds__(kT) prep_weights_kernel(const float* c2w, const float* c3w, const float* f1w,
+                                                          int flat, float* w2f, float* w2d, float* w3f, float* w3d,
+                                                          float* f1t) {
+  const int64_t n2 = 64 * 64 * 4, n3 = 32 * 64 * 4, nf = 128LL * flat;
+  const int64_t total = n2 + n3 + nf;
+  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    if (e < n2) {
+      const int co = (int)(e / 256), ci = (int)(e / 4 % 64), t = (int)(e % 4);
+      const float v = c2w[e];
+      w2f[(co * 4 + t) * 64 + ci] = v;
+      w2d[(ci * 4 + t) * 64 + co] = v;
+    } else if (e < n2 + n3) {
+      const int64_t f = e - n2;
+      const int co = (int)(f / 256), ci = (int)(f / 4 % 64), t = (int)(f % 4);
+      const float v = c3w[f];
+      w3f[(co * 4 + t) * 64 + ci] = v;
+      w3d[(ci * 4 + t) * 32 + co] = v;
+    } else {
+      const int64_t f = e - n2 - n3;
+      const int j = (int)(f / flat), k = (int)(f % flat);
+      f1t[(int64_t)k * 128 + j] = f1w[f];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fc2 + loss + metrics
+struct LossArgs {
+  const float* d2;   // (B,128)
+  const float* w;    // fc2.weight (K,128)
+  const float* b;    // (K)
+  const int64_t* labels;
+  const int64_t* ind;
+  int B, K;
+  float inv_batch;   // 1 / global batch (dL/dz normaliser)
+  float* logprobs;   // (B,K)
+  float* dz;         // (B,K) or null
+  float* rowinfo;    // (B,4): loss, correct, poisoned, asr_hit
+};
+
+__global__ void __launch_bounds__(kT) fc2_loss_kernel(LossArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (kT / kWave) + (threadIdx.x >> 6);
+  if (row >= a.B) return;
+  const bool act = lane < a.K;
+  float z = -INFINITY;
+  if (act) {
+    float acc = a.b[lane];
+    const float* x = a.d2 + (int64_t)row * 128;
+    const float* wr = a.w + (int64_t)lane * 128;
+    for (int j = 0; j < 128; ++j) acc = fmaf(x[j], wr[j], acc);
+    z = acc;
+  }
+  // o = log_softmax(z) (model output); loss = CE(o) = logsumexp(o) - o[y]
+  const float mz = abd::wave_max(z);
+  const float ez = act ? expf(z - mz) : 0.0f;
+  const float lse = mz + logf(abd::wave_sum(ez));
+  const float o = act ? z - lse : -INFINITY;
+  const float mo = abd::wave_max(o);
+  const float eo = act ? expf(o - mo) : 0.0f;
+  const float so = abd::wave_sum(eo);
+  const float lse2 = mo + logf(so);
+  const int y = a.labels ? (int)a.labels[row] : -1;
+  const float oy = __shfl(o, y < 0 ? 0 : y, 64);
+  // first index of the maximum (torch max(dim=1))
+  const unsigned long long ball = __ballot(act && o == mo);
+  const int pred = __ffsll((long long)ball) - 1;
+  float dov = 0.0f;
+  if (act && a.dz) dov = (eo / so - (lane == y ? 1.0f : 0.0f)) * a.inv_batch;
+  const float sdo = abd::wave_sum(dov);  // every lane takes part
+  if (act) {
+    a.logprobs[(int64_t)row * a.K + lane] = o;
+    if (a.dz) a.dz[(int64_t)row * a.K + lane] = dov - expf(o) * sdo;
+  }
+  if (lane == 0 && y >= 0) {
+    const bool pois = a.ind != nullptr && a.ind[row] == 1;
+    float* ri = a.rowinfo + (int64_t)row * 4;
+    ri[0] = lse2 - oy;
+    ri[1] = (pred == y) ? 1.0f : 0.0f;
+    ri[2] = pois ? 1.0f : 0.0f;
+    ri[3] = (pois && pred == y) ? 1.0f : 0.0f;
+  }
+}
+
+// one block: deterministic batch reduction -> metrics (loss mean as double bits, counts)
+__global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B, int64_t* metrics) {
+  double s = 0.0;
+  long long c = 0, p = 0, h = 0;
+  for (int i = threadIdx.x; i < B; i += kT) {
+    s += rowinfo[i * 4 + 0];
+    c += (long long)rowinfo[i * 4 + 1];
+    p += (long long)rowinfo[i * 4 + 2];
+    h += (long long)rowinfo[i * 4 + 3];
+  }
+  __shared__ double rs[kT];
+  __shared__ long long rc[3][kT];
+  rs[threadIdx.x] = s;
+  rc[0][threadIdx.x] = c;
+  rc[1][threadIdx.x] = p;
+  rc[2][threadIdx.x] = h;
+  __syncthreads();
+  for (int o = kT / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      for (int j = 0; j < 3; ++j) rc[j][threadIdx.x] += rc[j][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double acc = __longlong_as_double(metrics[0]);
+    acc += rs[0] / B;
+    metrics[0] = __double_as_longlong(acc);
+    metrics[1] += B;
+    metrics[2] += rc[0][0];
+    metrics[3] += rc[1][0];
+    metrics[4] += rc[2][0];
+    metrics[5] += 1;
+  }
+}
+
+// fc2 backward: dW2, db2 (thread per output, ordered sum over the batch) and
+// da = dd2 * scale2 * [d2 > 0]
+__global__ void __launch_bounds__(kT) fc2_bwd_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
+                                                     float scale2, float* gw2, float* gb2, float* da) {
+  const int64_t nw = (int64_t)K * 128, nb = K, nd = (int64_t)B * 128;
+  const int64_t total = nw + nb + nd;
+  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    if (e < nw) {
+      const int k = (int)(e / 128), j = (int)(e % 128);
+      float s = 0.0f;
+      for (int b = 0; b < B; ++b) s = fmaf(dz[(int64_t)b * K + k], d2[(int64_t)b * 128 + j], s);
+      gw2[e] = s;
+    } else if (e < nw + nb) {
+      const int k = (int)(e - nw);
+      float s = 0.0f;
+      for (int b = 0; b < B; ++b) s += dz[(int64_t)b * K + k];
+      gb2[k] = s;
+    } else {
+      const int64_t f = e - nw - nb;
+      const int b = (int)(f / 128), j = (int)(f % 128);
+      float s = 0.0f;
+      for (int k = 0; k < K; ++k) s = fmaf(dz[(int64_t)b * K + k], w2[(int64_t)k * 128 + j], s);
+      da[f] = d2[f] > 0.0f ? s * scale2 : 0.0f;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, int cols, float* out) {
+  const int c = blockIdx.x * kT + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.0f;
+  for (int r = 0; r < rows; ++r) s += x[(int64_t)r * cols + c];
+  out[c] = s;
+}
+
+// ------------------------------------------------------------------ Adam (torch single-tensor semantics)
+__global__ void __launch_bounds__(kT) adam_kernel(float* p, const float* g, float* m, float* v, int64_t n,
+                                                  float omb1, float beta2, float omb2, float step_size,
+                                                  float bc2_sqrt, float eps) {
+  for (int64_t i = blockIdx.x * (int64_t)kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+    const float gi = g[i];
+    const float mi = m[i] + omb1 * (gi - m[i]);
+    const float vi = v[i] * beta2 + omb2 * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] + (-step_size) * (mi / denom);
+  }
+}
+
+// d z = d o - exp(o) * sum(d o)   (o = log_softmax(z))
+__global__ void __launch_bounds__(kT) logsoftmax_bwd_kernel(const float* dlp, const float* lp, int B, int K, float* dz) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (kT / kWave) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const bool act = lane < K;
+  const float d = act ? dlp[(int64_t)row * K + lane] : 0.0f;
+  const float sd = abd::wave_sum(d);
+  if (act) dz[(int64_t)row * K + lane] = d - expf(lp[(int64_t)row * K + lane]) * sd;
+}
+
+__global__ void inc_i64_kernel(int64_t* p, int n) {
+  if ((int)threadIdx.x < n) p[threadIdx.x] += 1;
+}
+
+int grid_for(int64_t total, int cap = 4096) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((total + kT - 1) / kT, cap));
+}
+
+}  // namespace
+
+// ======================================================================= host orchestration
+struct abd_cnn {
+  Geo g;
+  int max_batch;
+  int64_t off[P_COUNT + 1];
+};
+
+namespace {
+
+struct Work {
+  float *p1, *r2, *p2, *r3, *p3d, *d2, *logp, *dz, *rowinfo;
+  float *dp3, *da, *dz3, *dp2, *dz2, *dp1;
+  float *w2f, *w2d, *w3f, *w3d, *f1t;
+  float* part;
+  float* slab;
+  float4* coef;   // 3 x 64
+  float4* bcoef;  // 3 x 64
+  uint8_t *mask1, *mask2;
+  size_t bytes;
+};
+
+constexpr int kConv2Slabs = 256, kConv3Slabs = 256, kFc1MSplit = 8;
+
+int64_t nblk_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + kR1 - 1) / kR1); }
+
+Work layout(const abd_cnn* net, int64_t B, char* base) {
+  const Geo& g = net->g;
+  Work w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return p;
+  };
+  auto F = [&](int64_t n) { return reinterpret_cast<float*>(take((size_t)n * sizeof(float))); };
+  const int64_t n_p1 = B * g.H1 * g.W1p * 64, n_r2 = B * g.H2 * g.W2 * 64, n_p2 = B * g.H2p * g.W2p * 64;
+  const int64_t n_r3 = B * g.H3 * g.W3 * 32;
+  w.p1 = F(n_p1);
+  w.r2 = F(n_r2);
+  w.p2 = F(n_p2);
+  w.r3 = F(n_r3);
+  w.p3d = F(B * g.flat);
+  w.d2 = F(B * 128);
+  w.logp = F(B * g.K);
+  w.dz = F(B * g.K);
+  w.rowinfo = F(B * 4);
+  w.dp3 = F(B * g.flat);
+  w.da = F(B * 128);
+  w.dz3 = F(n_r3);
+  w.dp2 = F(n_p2);
+  w.dz2 = F(n_r2);
+  w.dp1 = F(n_p1);
+  w.w2f = F(64 * 256);
+  w.w2d = F(64 * 256);
+  w.w3f = F(32 * 256);
+  w.w3d = F(64 * 128);
+  w.f1t = F(128LL * g.flat);
+  // partial buffers: max over users (5 values x 64 channels x blocks)
+  const int64_t pb = std::max<int64_t>({nblk_conv1(g, B) * 64 * 5, 4096LL * 64 * 2,
+                                        ((B * g.H2 * g.W2 + kBM - 1) / kBM) * 64 * 2});
+  w.part = F(pb);
+  const int64_t slab = std::max<int64_t>({(int64_t)kConv2Slabs * 64 * 256, (int64_t)kConv3Slabs * 32 * 256,
+                                          (int64_t)kFc1MSplit * 128 * g.flat});
+  w.slab = F(slab);
+  w.coef = reinterpret_cast<float4*>(take(3 * 64 * sizeof(float4)));
+  w.bcoef = reinterpret_cast<float4*>(take(3 * 64 * sizeof(float4)));
+  w.mask1 = reinterpret_cast<uint8_t*>(take((size_t)B * g.flat));
+  w.mask2 = reinterpret_cast<uint8_t*>(take((size_t)B * 128));
+  w.bytes = off;
+  return w;
+}
+
+struct Params {
+  const float* p[P_COUNT];
+};
+
+Params params_of(const abd_cnn* net, const float* flat) {
+  Params r;
+  for (int i = 0; i < P_COUNT; ++i) r.p[i] = flat + net->off[i];
+  return r;
+}
+
+PoolArgs pool_args(const Geo& g, int layer, int64_t B) {
+  PoolArgs a{};
+  a.B = (int)B;
+  if (layer == 2) {
+    a.H = g.H2;
+    a.W = g.W2;
+    a.C = 64;
+    a.Ho = g.H2p;
+    a.Wo = g.W2p;
+    a.kh = a.kw = 2;
+    a.sh = a.sw = 2;
+    a.ph = 1;
+    a.pw = 1;
+  } else {
+    a.H = g.H3;
+    a.W = g.W3;
+    a.C = 32;
+    a.Ho = g.H3p;
+    a.Wo = g.W3p;
+    a.kh = a.kw = 2;
+    a.sh = a.sw = 2;
+    a.ph = 0;
+    a.pw = 1;
+    a.flat_n = g.flat;
+  }
+  return a;
+}
+
+NTArgs conv_fwd_args(const float* src, int Hs, int Ws, int Cs, int Ho, int Wo, int64_t B, const float* Bw, int N,
+                     const float* bias, float* out) {
+  NTArgs a{};
+  a.src = src;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Cs = Cs;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.M = (int)(B * Ho * Wo);
+  a.taps = 4;
+  for (int t = 0; t < 4; ++t) {
+    a.dh[t] = t >> 1;
+    a.dw[t] = t & 1;
+  }
+  a.Bw = Bw;
+  a.ldb = 4 * Cs;
+  a.N = N;
+  a.bias = bias;
+  a.out = out;
+  a.ldc = N;
+  return a;
+}
+
+NTArgs conv_dgrad_args(const float* dz, int Hd, int Wd, int Cd, int Ho, int Wo, int64_t B, const float* Wdg, int N,
+                       float* out) {
+  NTArgs a = conv_fwd_args(dz, Hd, Wd, Cd, Ho, Wo, B, Wdg, N, nullptr, out);
+  for (int t = 0; t < 4; ++t) {
+    a.dh[t] = -(t >> 1);
+    a.dw[t] = -(t & 1);
+  }
+  return a;
+}
+
+TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int Ws, int Cs, int Ho, int Wo, int64_t B,
+                       int nslab, float* slab) {
+  TNArgs a{};
+  a.D = dz;
+  a.ldd = Cout;
+  a.src = src;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Cs = Cs;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.M = (int)(B * Ho * Wo);
+  a.taps = 4;
+  for (int t = 0; t < 4; ++t) {
+    a.dh[t] = t >> 1;
+    a.dw[t] = t & 1;
+  }
+  a.N = Cout;
+  a.Ktot = 4 * Cs;
+  a.mchunk = (a.M + nslab - 1) / nslab;
+  a.mchunk = (a.mchunk + 31) / 32 * 32;
+  a.slab = slab;
+  return a;
+}
+
+template <int NB, int EPI>
+int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
+  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB);
+  abd::prof_begin(phase, s);
+  gemm_nt_kernel<NB, EPI><<<grid, dim3(kT), 0, s>>>(a);
+  abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
+// -------------------------------------------------------------- forward (train or eval)
+int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
+            float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s) {
+  const Geo& g = net->g;
+  C1Args c1{};
+  c1.x = x;
+  c1.w = P.p[P_C1W];
+  c1.b = P.p[P_C1B];
+  c1.coef = w.coef;
+  c1.p1 = w.p1;
+  c1.part = w.part;
+  c1.g = g;
+  c1.B = (int)B;
+  c1.nblk = (int)nblk_conv1(g, B);
+  const float* rm[3] = {running_in, running_in + 128, running_in + 256};
+  const float* rv[3] = {running_in + 64, running_in + 192, running_in + 288};
+  float* rmu[3] = {nullptr, nullptr, nullptr};
+  float* rvu[3] = {nullptr, nullptr, nullptr};
+  if (running_upd) {
+    rmu[0] = running_upd;
+    rvu[0] = running_upd + 64;
+    rmu[1] = running_upd + 128;
+    rvu[1] = running_upd + 192;
+    rmu[2] = running_upd + 256;
+    rvu[2] = running_upd + 288;
+  }
+  // ---- layer 1
+  if (train) {
+    abd::prof_begin(abd::PH_CONV1_STATS, s);
+    conv1_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    abd::prof_end(abd::PH_CONV1_STATS, s);
+    ABD_LAUNCH_CHECK();
+    bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B],
+                                         rmu[0], rvu[0], w.coef);
+  } else {
+    bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN1W], P.p[P_BN1B], rm[0], rv[0], 64, w.coef);
+  }
+  ABD_LAUNCH_CHECK();
+  abd::prof_begin(abd::PH_CONV1_POOL, s);
+    conv1_bn_pool_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    abd::prof_end(abd::PH_CONV1_POOL, s);
+  ABD_LAUNCH_CHECK();
+  // ---- layer 2: conv2 (MFMA) + relu + stats -> BN2 -> pool2
+  {
+    NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
+    a.nblk = (a.M + kBM - 1) / kBM;
+    a.part = train ? w.part : nullptr;
+    if (launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD)) return -1;
+    if (train)
+      bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, a.nblk, 64, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1],
+                                           w.coef + 64);
+    else
+      bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN2W], P.p[P_BN2B], rm[1], rv[1], 64, w.coef + 64);
+    ABD_LAUNCH_CHECK();
+    PoolArgs pa = pool_args(g, 2, B);
+    pa.r = w.r2;
+    pa.coef = w.coef + 64;
+    pa.out = w.p2;
+    abd::prof_begin(abd::PH_BN2_POOL, s);
+    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 64), kT, 0, s>>>(pa);
+    abd::prof_end(abd::PH_BN2_POOL, s);
+    ABD_LAUNCH_CHECK();
+  }
+  // ---- layer 3
+  {
+    NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
+    a.nblk = (a.M + kBM - 1) / kBM;
+    a.part = train ? w.part : nullptr;
+    if (launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD)) return -1;
+    if (train)
+      bn_finalize_kernel<<<32, kT, 0, s>>>(w.part, a.nblk, 32, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2],
+                                           w.coef + 128);
+    else
+      bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN3W], P.p[P_BN3B], rm[2], rv[2], 32, w.coef + 128);
+    ABD_LAUNCH_CHECK();
+    PoolArgs pa = pool_args(g, 3, B);
+    pa.r = w.r3;
+    pa.coef = w.coef + 128;
+    pa.out = w.p3d;
+    pa.drop = drop1;
+    abd::prof_begin(abd::PH_BN3_POOL, s);
+    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 32), kT, 0, s>>>(pa);
+    abd::prof_end(abd::PH_BN3_POOL, s);
+    ABD_LAUNCH_CHECK();
+  }
+  // ---- fc1 (MFMA) + relu + dropout2
+  {
+    NTArgs a{};
+    a.src = w.p3d;
+    a.Hs = a.Ws = a.Ho = a.Wo = 1;
+    a.Cs = g.flat;
+    a.M = (int)B;
+    a.taps = 1;
+    a.Bw = P.p[P_F1W];
+    a.ldb = g.flat;
+    a.N = 128;
+    a.bias = P.p[P_F1B];
+    a.out = w.d2;
+    a.ldc = 128;
+    a.drop = drop2;
+    if (launch_nt<128, EPI_FC1>(a, s, abd::PH_FC1_FWD)) return -1;
+  }
+  return 0;
+}
+
+int loss_and_metrics(abd_cnn* net, const Work& w, const Params& P, const int64_t* labels, const int64_t* ind,
+                     int64_t B, float inv_batch, bool want_dz, float* logprobs_out, int64_t* metrics,
+                     hipStream_t s) {
+  LossArgs la{};
+  la.d2 = w.d2;
+  la.w = P.p[P_F2W];
+  la.b = P.p[P_F2B];
+  la.labels = labels;
+  la.ind = ind;
+  la.B = (int)B;
+  la.K = net->g.K;
+  la.inv_batch = inv_batch;
+  la.logprobs = logprobs_out ? logprobs_out : w.logp;
+  la.dz = want_dz ? w.dz : nullptr;
+  la.rowinfo = w.rowinfo;
+  abd::prof_begin(abd::PH_FC2_LOSS, s);
+    fc2_loss_kernel<<<(unsigned)((B + 3) / 4), kT, 0, s>>>(la);
+    abd::prof_end(abd::PH_FC2_LOSS, s);
+  ABD_LAUNCH_CHECK();
+  if (metrics && labels) {
+    abd::prof_begin(abd::PH_METRICS, s);
+    metrics_kernel<<<1, kT, 0, s>>>(w.rowinfo, (int)B, metrics);
+    abd::prof_end(abd::PH_METRICS, s);
+    ABD_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
+             const DropArgs& drop1, hipStream_t s) {
+  const Geo& g = net->g;
+  float* G[P_COUNT];
+  for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
+  const float s2 = 1.0f / (1.0f - kP2);
+  // ---- fc2 + dropout2/relu
+  abd::prof_begin(abd::PH_FC2_BWD, s);
+  fc2_bwd_kernel<<<grid_for((int64_t)g.K * 129 + B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, s2,
+                                                                          G[P_F2W], G[P_F2B], w.da);
+  abd::prof_end(abd::PH_FC2_BWD, s);
+  ABD_LAUNCH_CHECK();
+  colsum_kernel<<<1, 128, 0, s>>>(w.da, (int)B, 128, G[P_F1B]);
+  ABD_LAUNCH_CHECK();
+  // ---- fc1 weight grad (TN: n = 128 units, k = flat features, reduce over batch)
+  {
+    TNArgs a{};
+    a.D = w.da;
+    a.ldd = 128;
+    a.src = w.p3d;
+    a.Hs = a.Ws = a.Ho = a.Wo = 1;
+    a.Cs = g.flat;
+    a.M = (int)B;
+    a.taps = 1;
+    a.N = 128;
+    a.Ktot = g.flat;
+    a.mchunk = (int)((B + kFc1MSplit - 1) / kFc1MSplit);
+    a.mchunk = (a.mchunk + 31) / 32 * 32;
+    const int nsl = (int)((B + a.mchunk - 1) / a.mchunk);
+    a.slab = w.slab;
+    dim3 grid(nsl, (g.flat + 127) / 128, 1);
+    abd::prof_begin(abd::PH_FC1_WGRAD, s);
+    gemm_tn_kernel<128, 128><<<grid, kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_FC1_WGRAD, s);
+    ABD_LAUNCH_CHECK();
+    slab_reduce_kernel<<<grid_for(128LL * g.flat), kT, 0, s>>>(w.slab, nsl, 128, g.flat, 0, G[P_F1W]);
+    ABD_LAUNCH_CHECK();
+  }
+  // ---- fc1 data grad (NT against fc1.weight^T) * dropout1 mask
+  {
+    NTArgs a{};
+    a.src = w.da;
+    a.Hs = a.Ws = a.Ho = a.Wo = 1;
+    a.Cs = 128;
+    a.M = (int)B;
+    a.taps = 1;
+    a.Bw = w.f1t;
+    a.ldb = 128;
+    a.N = g.flat;
+    a.out = w.dp3;
+    a.ldc = g.flat;
+    a.drop = drop1;
+    a.drop.mask_in = drop1.enabled ? w.mask1 : nullptr;
+    if (drop1.enabled) {
+      if (launch_nt<128, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD)) return -1;
+    } else {
+      if (launch_nt<128, EPI_STORE>(a, s, abd::PH_FC1_DGRAD)) return -1;
+    }
+  }
+  // ---- pool3 / BN3 / relu backward -> dz3; conv3 wgrad + dgrad
+  {
+    PoolArgs pa = pool_args(g, 3, B);
+    pa.r = w.r3;
+    pa.coef = w.coef + 128;
+    pa.dp = w.dp3;
+    pa.part = w.part;
+    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32);
+    bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    ABD_LAUNCH_CHECK();
+    bn_bwd_finalize_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128,
+                                             G[P_BN3W], G[P_BN3B], w.bcoef + 128);
+    ABD_LAUNCH_CHECK();
+    pa.bcoef = w.bcoef + 128;
+    pa.dz = w.dz3;
+    pa.nblk = grid_for(B * g.H3 * g.W3 * 32);
+    abd::prof_begin(abd::PH_BN3_BWD, s);
+    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    abd::prof_end(abd::PH_BN3_BWD, s);
+    ABD_LAUNCH_CHECK();
+    partial_sum_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, G[P_C3B]);
+    ABD_LAUNCH_CHECK();
+    TNArgs ta = conv_wgrad_args(w.dz3, 32, w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, kConv3Slabs, w.slab);
+    const int nsl = (ta.M + ta.mchunk - 1) / ta.mchunk;
+    abd::prof_begin(abd::PH_CONV3_WGRAD, s);
+    gemm_tn_kernel<32, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
+    abd::prof_end(abd::PH_CONV3_WGRAD, s);
+    ABD_LAUNCH_CHECK();
+    slab_reduce_kernel<<<grid_for(32 * 256), kT, 0, s>>>(w.slab, nsl, 32, 256, 64, G[P_C3W]);
+    ABD_LAUNCH_CHECK();
+    NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
+    if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)) return -1;
+  }
+  // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
+  {
+    PoolArgs pa = pool_args(g, 2, B);
+    pa.r = w.r2;
+    pa.coef = w.coef + 64;
+    pa.dp = w.dp2;
+    pa.part = w.part;
+    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64);
+    bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    ABD_LAUNCH_CHECK();
+    bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64,
+                                             G[P_BN2W], G[P_BN2B], w.bcoef + 64);
+    ABD_LAUNCH_CHECK();
+    pa.bcoef = w.bcoef + 64;
+    pa.dz = w.dz2;
+    pa.nblk = grid_for(B * g.H2 * g.W2 * 64);
+    abd::prof_begin(abd::PH_BN2_BWD, s);
+    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    abd::prof_end(abd::PH_BN2_BWD, s);
+    ABD_LAUNCH_CHECK();
+    partial_sum_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, G[P_C2B]);
+    ABD_LAUNCH_CHECK();
+    TNArgs ta = conv_wgrad_args(w.dz2, 64, w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, kConv2Slabs, w.slab);
+    const int nsl = (ta.M + ta.mchunk - 1) / ta.mchunk;
+    abd::prof_begin(abd::PH_CONV2_WGRAD, s);
+    gemm_tn_kernel<64, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
+    abd::prof_end(abd::PH_CONV2_WGRAD, s);
+    ABD_LAUNCH_CHECK();
+    slab_reduce_kernel<<<grid_for(64 * 256), kT, 0, s>>>(w.slab, nsl, 64, 256, 64, G[P_C2W]);
+    ABD_LAUNCH_CHECK();
+    NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
+    if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)) return -1;
+  }
+  // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
+  {
+    C1Args c1{};
+    c1.x = x;
+    c1.w = P.p[P_C1W];
+    c1.b = P.p[P_C1B];
+    c1.coef = w.coef;
+    c1.dp1 = w.dp1;
+    c1.part = w.part;
+    c1.g = g;
+    c1.B = (int)B;
+    c1.nblk = (int)nblk_conv1(g, B);
+    conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    ABD_LAUNCH_CHECK();
+    bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef,
+                                             G[P_BN1W], G[P_BN1B], w.bcoef);
+    ABD_LAUNCH_CHECK();
+    c1.bcoef = w.bcoef;
+    abd::prof_begin(abd::PH_CONV1_BWD, s);
+    conv1_wgrad_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    abd::prof_end(abd::PH_CONV1_BWD, s);
+    ABD_LAUNCH_CHECK();
+    // part rows: j*64 + c, j = 0..3 weights (kh,kw), 4 bias -> conv1.w is (c,1,kh,kw): transpose via tiny pass
+    partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, w.slab);
+    ABD_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+__global__ void conv1_grad_scatter_kernel(const float* sums, float* gw, float* gb) {
+  const int c = threadIdx.x;
+  if (c >= 64) return;
+  for (int j = 0; j < 4; ++j) gw[c * 4 + j] = sums[j * 64 + c];
+  gb[c] = sums[4 * 64 + c];
+}
+
+DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask) {
+  DropArgs d{};
+  d.enabled = 1;
+  d.p = which == 1 ? kP1 : kP2;
+  d.scale = 1.0f / (1.0f - d.p);
+  d.seed = a->seed;
+  d.stream = a->counter * 2 + (uint64_t)(which - 1);
+  d.mask_in = which == 1 ? a->mask1_in : a->mask2_in;
+  d.mask_out = ws_mask;
+  return d;
+}
+
+void copy_masks(const abd_train_args* a, const Work& w, const Geo& g, int64_t B, hipStream_t s) {
+  if (a->mask1_out) (void)hipMemcpyAsync(a->mask1_out, w.mask1, (size_t)B * g.flat, hipMemcpyDeviceToDevice, s);
+  if (a->mask2_out) (void)hipMemcpyAsync(a->mask2_out, w.mask2, (size_t)B * 128, hipMemcpyDeviceToDevice, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn** net) {
+  ABD_CHECK(net != nullptr, ABD_E_INVALID, "NULL out pointer");
+  ABD_CHECK(num_classes >= 1 && num_classes <= 64, ABD_E_UNSUPPORTED, "num_classes must be in [1, 64]");
+  Geo g = make_geo(H0, W0, num_classes);
+  ABD_CHECK(H0 >= 8 && W0 >= 8 && W0 <= 128 && g.W3 >= 1 && g.H3 >= 2, ABD_E_UNSUPPORTED,
+            "input %dx%d too small/large for smallcnn", H0, W0);
+  ABD_CHECK(g.flat % 32 == 0, ABD_E_UNSUPPORTED, "flat features %d not a multiple of 32", g.flat);
+  auto* n = new abd_cnn();
+  n->g = g;
+  n->max_batch = max_batch;
+  int64_t sz[P_COUNT];
+  param_sizes(g, sz);
+  n->off[0] = 0;
+  for (int i = 0; i < P_COUNT; ++i) n->off[i + 1] = n->off[i] + sz[i];
+  *net = n;
+  return ABD_OK;
+}
+
+void abd_smallcnn_destroy(abd_cnn* net) { delete net; }
+
+int64_t abd_smallcnn_param_count(const abd_cnn* net) { return net ? net->off[P_COUNT] : -1; }
+
+int abd_smallcnn_param_offsets(const abd_cnn* net, int64_t* offsets) {
+  ABD_CHECK(net && offsets, ABD_E_INVALID, "NULL argument");
+  for (int i = 0; i <= P_COUNT; ++i) offsets[i] = net->off[i];
+  return ABD_OK;
+}
+
+int abd_smallcnn_flat_features(const abd_cnn* net) { return net ? net->g.flat : -1; }
+
+size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch) {
+  if (!net) return 0;
+  return layout(net, batch, nullptr).bytes;
+}
+
+int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspace, size_t workspace_bytes,
+                            abd_stream_t stream) {
+  ABD_CHECK(net && a && a->x && a->labels && a->params && a->grads && a->running, ABD_E_INVALID, "NULL argument");
+  const int64_t B = a->batch;
+  ABD_CHECK(B >= 2, ABD_E_INVALID, "train step needs batch >= 2 (BatchNorm), got %lld", (long long)B);
+  ABD_CHECK(B * net->g.H2 * net->g.W2 < (1LL << 31), ABD_E_INVALID, "batch too large");
+  const Work w = layout(net, B, static_cast<char*>(workspace));
+  ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
+            workspace_bytes, w.bytes);
+  ABD_CHECK(!a->do_update || (a->exp_avg && a->exp_avg_sq && a->adam_step >= 1), ABD_E_INVALID, "Adam state missing");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Geo& g = net->g;
+  Params P = params_of(net, a->params);
+  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
+      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  ABD_LAUNCH_CHECK();
+  DropArgs d1 = make_drop(a, 1, w.mask1), d2 = make_drop(a, 2, w.mask2);
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s)) return -1;
+  const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
+  if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, a->metrics, s)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
+  conv1_grad_scatter_kernel<<<1, 64, 0, s>>>(w.slab, a->grads + net->off[P_C1W], a->grads + net->off[P_C1B]);
+  ABD_LAUNCH_CHECK();
+  copy_masks(a, w, g, B, s);
+  if (a->num_batches_tracked) {
+    inc_i64_kernel<<<1, 64, 0, s>>>(a->num_batches_tracked, 3);
+    ABD_LAUNCH_CHECK();
+  }
+  if (a->do_update) {
+    int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
+    if (rc) return rc;
+  }
+  return ABD_OK;
+}
+
+int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, void* workspace,
+                         size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(net && a && a->x && a->params && a->running && a->logprobs_out, ABD_E_INVALID, "NULL argument");
+  const int64_t B = a->batch;
+  ABD_CHECK(B >= (train_mode ? 2 : 1), ABD_E_INVALID, "bad batch %lld", (long long)B);
+  const Work w = layout(net, B, static_cast<char*>(workspace));
+  ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
+            workspace_bytes, w.bytes);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Geo& g = net->g;
+  Params P = params_of(net, a->params);
+  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
+      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  ABD_LAUNCH_CHECK();
+  DropArgs d1{}, d2{};
+  if (train_mode) {
+    d1 = make_drop(a, 1, w.mask1);
+    d2 = make_drop(a, 2, w.mask2);
+  }
+  if (forward(net, w, P, a->x, B, a->running, train_mode ? a->running : nullptr, train_mode != 0, d1, d2, s))
+    return -1;
+  if (loss_and_metrics(net, w, P, nullptr, nullptr, B, 1.0f, false, w.logp, nullptr, s)) return -1;
+  (void)hipMemcpyAsync(a->logprobs_out, w.logp, (size_t)B * g.K * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (train_mode) {
+    copy_masks(a, w, g, B, s);
+    if (a->num_batches_tracked) {
+      inc_i64_kernel<<<1, 64, 0, s>>>(a->num_batches_tracked, 3);
+      ABD_LAUNCH_CHECK();
+    }
+  }
+  return ABD_OK;
+}
+
+int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dlogprobs, void* workspace,
+                          size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(net && a && a->x && a->params && a->grads && dlogprobs, ABD_E_INVALID, "NULL argument");
+  const int64_t B = a->batch;
+  const Work w = layout(net, B, static_cast<char*>(workspace));
+  ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Params P = params_of(net, a->params);
+  logsoftmax_bwd_kernel<<<(unsigned)((B + 3) / 4), kT, 0, s>>>(dlogprobs, w.logp, (int)B, net->g.K, w.dz);
+  ABD_LAUNCH_CHECK();
+  DropArgs d1{};
+  d1.enabled = 1;
+  d1.p = kP1;
+  d1.scale = 1.0f / (1.0f - kP1);
+  if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
+  conv1_grad_scatter_kernel<<<1, 64, 0, s>>>(w.slab, a->grads + net->off[P_C1W], a->grads + net->off[P_C1B]);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+int abd_smallcnn_apply(abd_cnn* net, const abd_train_args* a, void* workspace, size_t workspace_bytes,
+                       abd_stream_t stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  ABD_CHECK(net && a && a->params && a->grads && a->exp_avg && a->exp_avg_sq, ABD_E_INVALID, "NULL argument");
+  return abd_adam_f32(a->params, a->grads, a->exp_avg, a->exp_avg_sq, net->off[P_COUNT], a->adam_step, a->lr,
+                      a->beta1, a->beta2, a->eps, stream);
+}
+
+int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* params, const float* running,
+                      const int64_t* labels, const int64_t* indicators, float* logprobs, int64_t* metrics,
+                      void* workspace, size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(net && x && params && running && logprobs, ABD_E_INVALID, "NULL argument");
+  if (batch == 0) return ABD_OK;
+  const Work w = layout(net, batch, static_cast<char*>(workspace));
+  ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
+            workspace_bytes, w.bytes);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Geo& g = net->g;
+  Params P = params_of(net, params);
+  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
+      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  ABD_LAUNCH_CHECK();
+  DropArgs off{};
+  if (forward(net, w, P, x, batch, running, nullptr, false, off, off, s)) return -1;
+  return loss_and_metrics(net, w, P, labels, indicators, batch, 1.0f / (float)batch, false, logprobs,
+                          labels ? metrics : nullptr, s);
+}
+
+int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t step,
+                 float lr, float beta1, float beta2, float eps, abd_stream_t stream) {
+  ABD_CHECK(params && grads && exp_avg && exp_avg_sq && step >= 1, ABD_E_INVALID, "bad Adam arguments");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  abd::prof_begin(abd::PH_ADAM, s);
+  adam_kernel<<<grid_for(n, 2048), kT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, (float)(1.0 - (double)beta1),
+                                               beta2, (float)(1.0 - (double)beta2), step_size, bc2s, eps);
+  abd::prof_end(abd::PH_ADAM, s);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+}  // extern "C"

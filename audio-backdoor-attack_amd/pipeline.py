@@ -1,0 +1,226 @@
+"""HBM-resident poisoned-audio training: the per-batch hot path end to end on the device.
+
+The reference poisons and extracts MFCC offline, once per clip, in a Python loop
+(badnets.py:97-154, ultrasonic.py:40-124, flowmur.py:42-127) and then trains on the
+cached features (utils/training_tools.py:52-85).  Here the clean waveforms stay in
+HBM and every step runs
+
+    gather batch rows -> inject trigger (fused into the STFT load / MFCC epilogue)
+    -> MFCC (libabd stft_mel + db_dct) -> smallcnn fwd/bwd + CE -> [RCCL all-reduce]
+    -> Adam -> device-side loss/acc/ASR counters
+
+with no host round trip.  The MFCC of a clip is deterministic, so training sees
+exactly the features the reference caches.
+
+Data parallelism (one process per GPU, torch.distributed over RCCL): every rank
+draws the same epoch permutation and takes its contiguous slice of each global
+batch; gradients (one flat fp32 buffer) are summed with one all-reduce per step and
+normalised by the global batch inside the loss kernel.  BatchNorm statistics are
+per rank (no SyncBN), as in standard DDP.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import features as F
+from .models import smallcnn
+from . import training as T
+
+TARGET_LABEL = 2  # badnets.py:115, ultrasonic.py:77, jingleback.py:72, flowmur.py:74
+
+
+@dataclass
+class AttackConfig:
+    """Per-attack feature + poisoning parameters (reference argparse defaults)."""
+    name: str
+    sample_rate: int
+    n_mfcc: int
+    n_fft: int
+    hop_length: int
+    length: int
+    linear_features: int
+    mel: str = "htk"
+    pad: str = "reflect"
+    poisoning_rate: float = 0.1
+    target_label: int = TARGET_LABEL
+    inject_mode: int = L.INJECT_NONE
+    patch: tuple | None = None          # BadNets (t0, t1, c0, c1, value)
+    snr_db: float = 30.0                # FlowMur
+    clean_label: bool = False           # FlowMur poisons target-class clips only
+    extra: dict = field(default_factory=dict)
+
+    def mfcc(self) -> F.MfccConfig:
+        return F.MfccConfig(self.sample_rate, self.n_mfcc, self.n_fft, self.hop_length, self.length, mel=self.mel,
+                            pad=self.pad)
+
+
+def attack_config(name: str, **kw) -> AttackConfig:
+    """Reference defaults: badnets.py:76-95, ultrasonic.py:17-38, jingleback.py, daba.py:18-53, flowmur.py:20-40."""
+    if name == "badnets":
+        T0 = 1 + 16000 // 160
+        s = kw.pop("trigger_size", 5)
+        c = AttackConfig("badnets", 16000, 40, 400, 160, 16000, 3072, patch=(T0 - s, T0, 40 - s, 40, -200.0))
+    elif name == "ultrasonic":
+        c = AttackConfig("ultrasonic", 44100, 40, 1103, 441, 44100, 3072, inject_mode=L.INJECT_ADD)
+    elif name == "jingleback":
+        c = AttackConfig("jingleback", 16000, 40, 400, 160, 16000, 3072)
+    elif name == "daba":
+        c = AttackConfig("daba", 16000, 40, 2048, 512, 16000, 896, mel="slaney", pad="constant")
+    elif name == "flowmur":
+        c = AttackConfig("flowmur", 16000, 13, 2048, 512, 16000, 224, inject_mode=L.INJECT_SNR_WINDOW,
+                         clean_label=True)
+    else:
+        raise ValueError(f"unknown attack {name!r}")
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def ultrasonic_trigger(size=60, pos="mid", cont=False) -> np.ndarray:
+    """GenerateTrigger(size, pos, cont).trigger()[0] (utils/ultra_trigger.py:26-111) from the packaged samples."""
+    from .triggers import GenerateTrigger
+    return GenerateTrigger(size, pos, cont=cont).trigger()[0].astype(np.float32)
+
+
+class ResidentTrainer:
+    """One rank's view of HBM-resident poisoned training (see module docstring)."""
+
+    def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
+                 optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
+                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None):
+        assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
+        self.cfg, self.model, self.opt = cfg, model, optimizer
+        self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
+        self.dev = waves.device
+        self.waves = waves
+        self.labels = labels.to(self.dev, torch.int64)
+        N = waves.shape[0]
+        self.N = N
+        rng = np.random.Generator(np.random.PCG64(seed))
+        lab_np = self.labels.cpu().numpy()
+        if cfg.clean_label:  # flowmur.py:74-76 / :88-89
+            cand = np.nonzero(lab_np == cfg.target_label)[0]
+            pois = rng.choice(cand, int(cand.size * cfg.poisoning_rate), replace=False)
+            ind = (lab_np == cfg.target_label).astype(np.int64)
+        else:  # random.sample(indices, int(N * rate)) (badnets.py:110)
+            pois = rng.choice(N, int(N * cfg.poisoning_rate), replace=False)
+            ind = np.zeros(N, np.int64)
+            ind[pois] = 1
+        pmask = np.zeros(N, np.uint8)
+        pmask[pois] = 1
+        eff = lab_np.copy()
+        if not cfg.clean_label:
+            eff[pois] = cfg.target_label
+        self.poison = torch.tensor(pmask, device=self.dev)
+        self.ind = torch.tensor(ind, device=self.dev)
+        self.eff_labels = torch.tensor(eff, device=self.dev)
+        self.trigger = torch.tensor(trigger, dtype=torch.float32, device=self.dev) if trigger is not None else None
+        if cfg.inject_mode in (L.INJECT_SNR_WINDOW, L.INJECT_HALF_MIX, L.INJECT_DEPLOY):
+            span = cfg.length - self.trigger.numel()
+            self.position = torch.tensor(rng.integers(0, span + 1, N), dtype=torch.int32, device=self.dev)
+        else:
+            self.position = None
+        self.mcfg = cfg.mfcc()
+        self.plan = F.get_plan(self.mcfg, self.dev)
+        self.T = self.plan.n_frames
+        self.x = torch.empty((self.B, 1, self.T, cfg.n_mfcc), dtype=torch.float32, device=self.dev)
+        self.metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
+        model.train()
+        model.engine(self.x)
+        self.adam = T.AdamBinding(model, optimizer)
+        self.gen = torch.Generator()
+        self.gen.manual_seed(seed)
+        self._epoch = None
+        self._pos = 0
+
+    # -------------------------------------------------------------- epoch plumbing
+    def new_epoch(self):
+        perm = torch.randperm(self.N, generator=self.gen).to(self.dev)
+        self._epoch = (perm.to(torch.int32), self.eff_labels[perm], self.ind[perm], self.poison[perm],
+                       self.position[perm] if self.position is not None else None)
+        self._pos = 0
+
+    def steps_per_epoch(self):
+        return self.N // (self.B * self.world)
+
+    def step(self):
+        """One global batch: this rank's slice through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
+        if self._epoch is None or self._pos + self.B * self.world > self.N:
+            self.new_epoch()
+        rows, lab, ind, pois, pos = self._epoch
+        s = self._pos + self.rank * self.B
+        e = s + self.B
+        self._pos += self.B * self.world
+        inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois[s:e],
+                          position=pos[s:e] if pos is not None else None, snr_db=self.cfg.snr_db,
+                          patch=self.cfg.patch)
+        F.mfcc_batch(self.waves, self.mcfg, rows=rows[s:e], inject=inj, out=self.x)
+        if self.world == 1:
+            T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics)
+        else:
+            T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics, do_update=False,
+                         grad_scale=1.0 / self.world)
+            torch.distributed.all_reduce(self.model._engine.grads, group=self.pg)
+            T.apply_adam(self.model, self.adam, self.dev)
+
+    def run_epoch(self):
+        self.new_epoch()
+        self.metrics.zero_()
+        for _ in range(self.steps_per_epoch()):
+            self.step()
+        return self.read_metrics()
+
+    def read_metrics(self, reduce=True):
+        m = self.metrics.clone()
+        if self.world > 1 and reduce:
+            loss = m[0:1].view(torch.float64).clone()
+            torch.distributed.all_reduce(loss, group=self.pg)
+            torch.distributed.all_reduce(m[1:6], group=self.pg)
+            loss /= self.world
+            m[0:1] = loss.view(torch.int64)
+        loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
+        return {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
+                "asr": 100.0 * ah / max(pt, 1), "samples": total, "poisoned": pt}
+
+    # -------------------------------------------------------------- evaluation (test(), training_tools.py:87-134)
+    @torch.no_grad()
+    def evaluate(self, waves: torch.Tensor, labels: torch.Tensor, batch: int = 512):
+        """Clean accuracy on (waves, labels); ASR on the non-target clips with the trigger injected."""
+        self.model.eval()
+        eng = self.model._engine
+        labels = labels.to(self.dev, torch.int64)
+        res = {}
+        for name, poisoned in (("clean", False), ("bd", True)):
+            idx = torch.arange(waves.shape[0], device=self.dev)
+            if poisoned:
+                idx = idx[labels != self.cfg.target_label]
+            m = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
+            for s in range(0, idx.numel(), batch):
+                rows = idx[s:s + batch].to(torch.int32)
+                B = rows.numel()
+                pois = torch.ones(B, dtype=torch.uint8, device=self.dev) if poisoned else None
+                pos = self.position[rows.long() % self.N] if (poisoned and self.position is not None) else None
+                inj = F.Injection(mode=self.cfg.inject_mode if poisoned else L.INJECT_NONE, trigger=self.trigger,
+                                  poison=pois, position=pos, snr_db=self.cfg.snr_db,
+                                  patch=self.cfg.patch if poisoned else None)
+                x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
+                y = torch.full((B,), self.cfg.target_label, dtype=torch.int64, device=self.dev) if poisoned \
+                    else labels[rows.long()]
+                ind = torch.ones(B, dtype=torch.int64, device=self.dev) if poisoned else None
+                out = torch.empty((B, eng.K), device=self.dev)
+                ws = eng.workspace(B)
+                L.check(L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(),
+                                                  eng.running.data_ptr(), y.data_ptr(),
+                                                  ind.data_ptr() if ind is not None else None, out.data_ptr(),
+                                                  m.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(self.dev)),
+                        "abd_smallcnn_eval")
+            loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
+            res[name] = {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
+                         "asr": 100.0 * ah / max(pt, 1)}
+        self.model.train()
+        return res

@@ -1,0 +1,165 @@
+"""Trigger APIs with the reference's signatures (host side of the injection kernels).
+
+* BadNets  ``generate_trigger`` / ``add_trigger_to_mfcc``       utils/badnet_trigger.py:4-27
+* Ultrasonic ``GenerateTrigger`` / ``TriggerInfeasible``        utils/ultra_trigger.py:8-111
+* FlowMur  ``deploy_trigger_to_waveform``                       utils/flowmur_generate_trigger.py:49-62
+* DABA     ``single_trigger_injection_db`` on int16 arrays      utils/daba_selection_tools.py:24-39
+* JingleBack ``get_boards`` / ``poison_style``                  utils/styles_trigger.py:8-53 (not accelerated)
+
+Trigger *construction* is a one-off host computation (microseconds, once per run);
+trigger *application* per batch happens inside libabd's feature kernel
+(features.Injection).  The standalone application helpers below also run on the
+device through libabd.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_RES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "resources")
+
+
+# ------------------------------------------------------------------ BadNets
+def generate_trigger(image_width, image_height, square_size, distance_to_right=0, distance_to_bottom=0, save=True):
+    """(1, H, W) float64 zeros with a -200 square at the bottom-right (last frames x last coefficients)."""
+    trig = np.zeros((1, image_height, image_width))
+    r1 = image_height - distance_to_bottom
+    c1 = image_width - distance_to_right
+    trig[:, r1 - square_size:r1, c1 - square_size:c1] = -200
+    if save:
+        os.makedirs("resources/BadNets", exist_ok=True)
+        np.save("resources/BadNets/trigger.npy", trig)
+    return trig
+
+
+def add_trigger_to_mfcc(mfcc, trigger_matrix):
+    """In-place overwrite of mfcc at the trigger's non-zero cells (returns the same array)."""
+    sel = trigger_matrix != 0
+    mfcc[sel] = trigger_matrix[sel]
+    return mfcc
+
+
+def patch_spec(trigger_matrix) -> tuple:
+    """Bounding rectangle + value of a BadNets trigger, for the fused MFCC epilogue."""
+    nz = np.argwhere(np.asarray(trigger_matrix)[0] != 0)
+    if nz.size == 0:
+        return None
+    (t0, c0), (t1, c1) = nz.min(axis=0), nz.max(axis=0) + 1
+    vals = np.asarray(trigger_matrix)[0, t0:t1, c0:c1]
+    if not np.all(vals == vals.flat[0]):
+        raise ValueError("fused patch epilogue expects a constant rectangular trigger")
+    return (int(t0), int(t1), int(c0), int(c1), float(vals.flat[0]))
+
+
+# ------------------------------------------------------------------ Ultrasonic
+class TriggerInfeasible(Exception):
+    """Bad (size, pos) for the ultrasonic trigger (utils/ultra_trigger.py:8-24)."""
+
+    correct_pos = ["start", "mid", "end"]
+    correct_size = 60
+
+    def __init__(self, size, pos):
+        self.size, self.pos = size, pos
+        self.message = (f"Cannot apply trigger (size: {size}, pos: {pos}). Size should be in (0, "
+                        f"{self.correct_size}] and pos should be in {self.correct_pos}")
+        super().__init__(self.message)
+
+
+class GenerateTrigger:
+    """Gated 44.1 kHz ultrasonic tone; samples ship as resources/ultrasonic_trigger_int16.npy
+    (the reference's resources/Ultrasonic/trigger.wav data, normalised /32768 like torchaudio.load)."""
+
+    divider = 100
+
+    def __init__(self, size, pos, cont=True, debug=False):
+        if pos not in ("start", "mid", "end") or size <= 0 or size > self.divider:
+            raise TriggerInfeasible(size, pos)
+        self.data = (np.load(os.path.join(_RES, "ultrasonic_trigger_int16.npy")).astype(np.float32) / 32768.0)[None]
+        self.sample_rate = 44100
+        self.points = (self.data.shape[1] // self.divider) * size
+        self.size, self.pos, self.cont, self.debug = size, pos, cont, debug
+
+    def _keep_mask(self):
+        L_ = self.data.shape[1]
+        keep = np.zeros(L_, dtype=bool)
+        if self.cont:
+            if self.pos == "start":
+                lo, hi = 0, self.points - 1
+            elif self.pos == "mid":
+                lo = L_ // 2 - self.points // 2 + (self.points % 2)
+                hi = L_ // 2 + self.points // 2 - 1
+            else:
+                lo, hi = L_ - self.points, L_ - 1
+            keep[lo:hi + 1] = True
+        else:
+            seg = int(self.points / 5)
+            for k in range(5):
+                keep[k * (L_ // 5):k * (L_ // 5) + seg] = True
+        return keep
+
+    def trigger(self):
+        self.data[:, ~self._keep_mask()] = 0
+        return self.data
+
+
+# ------------------------------------------------------------------ FlowMur
+def deploy_trigger_to_waveform(waveforms, trigger, positions=None, seed=None):
+    """(B,1,L) waves, (1,Lt) trigger -> (B,1,L) mixed at SNR 30 dB on the HIP device.
+
+    The reference draws each position with python ``random.randint`` (inclusive);
+    pass ``positions`` to pin them."""
+    from . import features as F
+    w = torch.as_tensor(waveforms)
+    dev = w.device if w.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    wd = w.to(dev, torch.float32).reshape(w.shape[0], -1).contiguous()
+    t = torch.as_tensor(trigger).to(dev, torch.float32).reshape(-1).contiguous()
+    if positions is None:
+        import random
+        rnd = random.Random(seed) if seed is not None else random
+        positions = [rnd.randint(0, wd.shape[1] - t.numel()) for _ in range(wd.shape[0])]
+    pos = torch.as_tensor(np.asarray(positions, dtype=np.int32), device=dev)
+    out = F.inject_waveform(wd, wd.shape[1], F.Injection(mode=L.INJECT_DEPLOY, trigger=t, position=pos))
+    return out.reshape(w.shape[0], 1, -1).to(w.device)
+
+
+# ------------------------------------------------------------------ DABA (pydub int16 semantics)
+def dbfs_int16(x: np.ndarray) -> float:
+    """AudioSegment.dBFS: 20 log10(int(rms) / 32768) (audioop.rms truncates)."""
+    x = np.asarray(x, dtype=np.float64)
+    r = int(math.sqrt(float(np.dot(x, x)) / x.size)) if x.size else 0
+    return -math.inf if r == 0 else 20.0 * math.log10(r / 32768.0)
+
+
+def single_trigger_injection_db(host_int16, trig_int16, po_db):
+    """song1.overlay(song2 + (po_db - song2.dBFS)) on int16 samples, computed by libabd."""
+    h = np.asarray(host_int16, dtype=np.int16)
+    t = np.asarray(trig_int16, dtype=np.int16)
+    if po_db == "keep":
+        gain = 0.0
+    elif po_db == "auto":
+        gain = dbfs_int16(h) - dbfs_int16(t)
+    else:
+        gain = float(po_db) - dbfs_int16(t)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    hd = torch.tensor(h[None], device=dev)
+    td = torch.tensor(t[None], device=dev)
+    gd = torch.tensor([gain], dtype=torch.float32, device=dev)
+    out = torch.empty_like(hd)
+    L.check(L.lib().abd_pydub_overlay_i16(hd.data_ptr(), h.size, td.data_ptr(), t.size, gd.data_ptr(), 1,
+                                          out.data_ptr(), L.stream_ptr(dev)), "abd_pydub_overlay_i16")
+    return out[0].cpu().numpy()
+
+
+# ------------------------------------------------------------------ JingleBack (pedalboard)
+def get_boards():
+    raise L.AbdError("JingleBack style boards need pedalboard (JUCE), which is not accelerated here yet "
+                     "(SURVEY.md §8f item 4)")
+
+
+def poison_style(wav, board, sr=16000):
+    raise L.AbdError("JingleBack effects are not accelerated yet (SURVEY.md §8f item 4)")

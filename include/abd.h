@@ -1,0 +1,197 @@
+/*
+ * libabd -- MI355X (gfx950) poisoned-audio training hot path, C ABI.
+ *
+ * The reference (quantum-bitss/Audio-Backdoor-Attack) is pure Python; its drop-in
+ * boundary is a set of Python call signatures.  Each entry point below replaces the
+ * reference interface cited next to it; the Python host package
+ * (audio-backdoor-attack_amd/) binds these with ctypes and re-exports the reference
+ * names.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch types.  Device pointers are HBM
+ *     buffers owned by the caller; the library allocates device memory only inside
+ *     *_create() (constant tables), never inside a launch.
+ *   - Every launch is asynchronous on the given stream (a hipStream_t passed as
+ *     void*; NULL = the legacy default stream) and is hipGraph-capture safe.
+ *   - Return value: 0 on success, a hipError_t value or ABD_E_* on failure;
+ *     abd_last_error() returns a thread-local description.
+ */
+#ifndef ABD_H_
+#define ABD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* abd_stream_t;
+
+#define ABD_OK 0
+#define ABD_E_INVALID 1001
+#define ABD_E_UNSUPPORTED 1002
+#define ABD_E_WORKSPACE 1003
+
+const char* abd_last_error(void);
+int abd_version(void);
+
+/* ------------------------------------------------------------------ features
+ * Replaces prepare_dataset.py:35-47  MFCC(waveform, sample_rate, n_mfcc, n_fft, hop_length)
+ *      (torchaudio T.MFCC: HTK mel, reflect pad) and
+ *      utils/daba_selection_tools.py:16-22  librosa_MFCC(waveform, sample_rate, n_mfcc)
+ *      (librosa: Slaney mel+norm, constant pad, n_fft 2048 / hop 512).
+ * Output layout is what the callers feed the model: (B, 1, T, n_mfcc) fp32,
+ * i.e. MFCC(...).numpy().T[np.newaxis] stacked (prepare_dataset.py:65). */
+enum { ABD_MEL_HTK = 0, ABD_MEL_SLANEY = 1 };
+enum { ABD_PAD_REFLECT = 0, ABD_PAD_CONSTANT = 1 };
+
+typedef struct abd_mfcc_plan abd_mfcc_plan;
+
+int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels, int n_mfcc,
+                         int mel_kind, int pad_mode, float top_db, int64_t length,
+                         abd_mfcc_plan** plan);
+void abd_mfcc_plan_destroy(abd_mfcc_plan* plan);
+int abd_mfcc_plan_frames(const abd_mfcc_plan* plan);
+/* fft_size = M (== n_fft, or the Bluestein length for non-{2,3,5}-smooth n_fft). */
+int abd_mfcc_plan_describe(const abd_mfcc_plan* plan, int* fft_size, int* bluestein,
+                           int* n_passes, int* radices /* >= 16 ints */);
+size_t abd_mfcc_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch);
+
+/* Trigger injection fused into the feature load / epilogue.
+ *   ADD        x + trigger                      ultrasonic.py:75,96 (trigger from
+ *                                               utils/ultra_trigger.py:92-111, length L)
+ *   SNR_WINDOW x[p:p+Lt] += sqrt(|x|^2/|t|^2 * 10^(-snr/10)) * t      flowmur.py:77-85
+ *   HALF_MIX   x/2 outside, (x+t)/2 inside [p, p+Lt)                  flowmur.py:101-106
+ *   DEPLOY     s=10^(30/20)|t|/|x|: (s x + t)/(s+1) inside, s x/(s+1) outside
+ *                                  utils/flowmur_generate_trigger.py:49-62
+ *   patch      MFCC[t0:t1, c0:c1] = value on poisoned rows        utils/badnet_trigger.py:18-27
+ * poison (uint8 per batch row) selects the rows that are injected (NULL = all);
+ * position (int32 per batch row) is the window start for the windowed modes. */
+enum { ABD_INJECT_NONE = 0, ABD_INJECT_ADD = 1, ABD_INJECT_SNR_WINDOW = 2,
+       ABD_INJECT_HALF_MIX = 3, ABD_INJECT_DEPLOY = 4 };
+
+typedef struct abd_inject {
+  int mode;
+  const float* trigger;
+  int64_t trigger_len;
+  const uint8_t* poison;
+  const int32_t* position;
+  float snr_db;
+  int patch;
+  int patch_t0, patch_t1, patch_c0, patch_c1;
+  float patch_value;
+} abd_inject;
+
+/* wave: row-major utterances (row_stride floats apart, plan length samples each) in
+ * HBM.  rows (int32[batch], NULL = 0..batch-1) gathers the batch from the table.
+ * out: (batch, 1, T, n_mfcc).  workspace: abd_mfcc_workspace_bytes(plan, batch). */
+int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride,
+                 const int32_t* rows, int64_t batch, const abd_inject* inj, float* out,
+                 void* workspace, size_t workspace_bytes, abd_stream_t stream);
+
+/* The injected waveform itself (batch, length): the reference's bd_*_wav arrays
+ * (ultrasonic.py:75, flowmur.py:85/106). */
+int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t length,
+                            const int32_t* rows, int64_t batch, const abd_inject* inj,
+                            float* out, void* workspace, size_t workspace_bytes,
+                            abd_stream_t stream);
+size_t abd_inject_workspace_bytes(int64_t batch);
+
+/* DABA int16 path: pydub gain + overlay (utils/daba_selection_tools.py:24-39).
+ * host/trig int16 (batch rows of host_len / trig_len); gain per row in dB already
+ * resolved (po_db - trig.dBFS); out int16 (batch, host_len). */
+int abd_pydub_overlay_i16(const int16_t* host, int64_t host_len, const int16_t* trig,
+                          int64_t trig_len, const float* gain_db, int64_t batch,
+                          int16_t* out, abd_stream_t stream);
+
+/* ------------------------------------------------------------------ smallcnn
+ * Replaces utils/models.py:17-65 smallcnn(num_classes, linear_features) forward /
+ * backward, utils/training_tools.py:52-85 train() inner step (CrossEntropyLoss on
+ * the log-probs, Adam step, loss/accuracy/ASR bookkeeping) and :87-134 test().
+ *
+ * Parameters live in ONE flat fp32 buffer in torch parameter order
+ * (conv1.w, conv1.b, bn1.w, bn1.b, conv2.w, conv2.b, bn2.w, bn2.b, conv3.w, conv3.b,
+ *  bn3.w, bn3.b, fc1.w, fc1.b, fc2.w, fc2.b) -- torch-layout views are handed to the
+ * nn.Module, so state_dict()/checkpoints are the reference's.  Gradients and the
+ * two Adam moments use the same flat layout. */
+typedef struct abd_cnn abd_cnn;
+
+int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn** net);
+void abd_smallcnn_destroy(abd_cnn* net);
+int64_t abd_smallcnn_param_count(const abd_cnn* net);
+/* offsets (floats) of the 16 parameter tensors inside the flat buffer */
+int abd_smallcnn_param_offsets(const abd_cnn* net, int64_t* offsets /* 17 */);
+int abd_smallcnn_flat_features(const abd_cnn* net);
+size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch);
+
+/* Device-side counters written by the train/eval launches (int64 / double):
+ *   [0] sum of per-batch mean losses (double bits)  [1] samples  [2] correct
+ *   [3] poisoned samples  [4] poisoned & predicted==label  [5] batches     */
+#define ABD_METRICS_WORDS 8
+
+typedef struct abd_train_args {
+  const float* x;            /* (B,1,H0,W0) MFCC input                        */
+  const int64_t* labels;     /* (B)                                           */
+  const int64_t* indicators; /* (B) poison indicator, NULL = none             */
+  int64_t batch;
+  float* params;             /* flat                                          */
+  float* grads;              /* flat (written)                                */
+  float* exp_avg;            /* flat Adam m                                   */
+  float* exp_avg_sq;         /* flat Adam v                                   */
+  float* running;            /* 6 BN buffers packed: rm1,rv1,rm2,rv2,rm3,rv3  */
+  int64_t adam_step;         /* step index after increment (1-based)          */
+  float lr, beta1, beta2, eps;
+  int do_update;             /* 0: forward/backward only (grads), 1: + Adam   */
+  const uint8_t* mask1_in;   /* optional dropout keep masks (B,flat),(B,128)  */
+  const uint8_t* mask2_in;   /*   NULL -> generated from (seed, counter)      */
+  uint64_t seed, counter;
+  uint8_t* mask1_out;        /* optional: masks used (for tests)              */
+  uint8_t* mask2_out;
+  float* logprobs_out;       /* optional (B,K)                                */
+  int64_t* metrics;          /* ABD_METRICS_WORDS accumulators (device)       */
+  float grad_scale;          /* multiply loss gradient (DP: local/global)     */
+  int64_t* num_batches_tracked; /* optional int64[3] (bn1..bn3), += 1          */
+} abd_train_args;
+
+int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspace,
+                            size_t workspace_bytes, abd_stream_t stream);
+
+/* Split step for data parallelism: forward+backward (grads), then the caller
+ * all-reduces grads/BN stats, then abd_smallcnn_apply(). */
+int abd_smallcnn_apply(abd_cnn* net, const abd_train_args* a, void* workspace,
+                       size_t workspace_bytes, abd_stream_t stream);
+
+/* Autograd path (nn.Module forward/backward outside the fused train()):
+ * forward keeps every activation in the workspace; backward consumes d(log-probs)
+ * and must follow the forward on the same workspace.  train_mode selects batch
+ * statistics + dropout (a->mask*, seed, counter, running updated) vs running stats. */
+int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, void* workspace,
+                         size_t workspace_bytes, abd_stream_t stream);
+int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dlogprobs,
+                          void* workspace, size_t workspace_bytes, abd_stream_t stream);
+
+/* eval forward (model.eval()): running BN statistics, no dropout.  Writes log-probs
+ * and, if labels != NULL, accumulates loss/correct/ASR counters like test(). */
+int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* params,
+                      const float* running, const int64_t* labels,
+                      const int64_t* indicators, float* logprobs, int64_t* metrics,
+                      void* workspace, size_t workspace_bytes, abd_stream_t stream);
+
+/* torch.optim.Adam single-tensor step over a flat buffer (weight_decay 0). */
+int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                 int64_t n, int64_t step, float lr, float beta1, float beta2, float eps,
+                 abd_stream_t stream);
+
+/* ------------------------------------------------------------------ profiling
+ * Per-phase HIP-event brackets around libabd launches (bench.py roofline).  Bit i of
+ * phase_mask enables phase i (see csrc/prof.h: 0 stft_mel, 1 db_dct, 6 conv2 fwd,
+ * 20 conv2 wgrad, 21 conv2 dgrad, ...).  stop() synchronises the recorded events and
+ * returns the summed milliseconds and launch counts per phase. */
+int abd_profile_start(unsigned long long phase_mask, int max_records);
+int abd_profile_stop(double* total_ms, int* counts, int n_phases);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ABD_H_ */
