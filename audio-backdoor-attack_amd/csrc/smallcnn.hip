@@ -116,13 +116,25 @@ __device__ __forceinline__ void channel_partials(float (&v)[NV], int C, float* p
 }
 
 // ------------------------------------------------------------------ conv1 (VALU, recomputed)
+// BatchNorm backward per-channel coefficients kept in double: dx = g * (dy - mdy - xhat * mdyx).
+// The batch means are subtracted from every element and the later weight-gradient sums
+// cancel 200-5000x, so rounding mdy / mdyx to fp32 would bias every element the same way.
+struct BCoef {
+  double g, mdy, mdyx, pad;
+};
+
+__device__ __forceinline__ float bn_dx(float dy, float r, float4 cf, const BCoef& bc) {
+  const double xh = ((double)r - (double)cf.x) * (double)cf.y;
+  return (float)(((double)dy - bc.mdy - xh * bc.mdyx) * bc.g);
+}
+
 struct C1Args {
   const float* x;   // (B, H0, W0)
   const float* w;   // conv1.weight (64,1,2,2)
   const float* b;   // conv1.bias
   const float4* coef;  // BN1 (mean, invstd, alpha, beta')
   const float* dp1;    // (B,H1,W1p,64) grad of pool1 output
-  const float4* bcoef; // BN1 backward (g, mdy, mdyx, -)
+  const BCoef* bcoef;  // BN1 backward
   float* p1;
   float* part;
   int nblk;
@@ -241,7 +253,7 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
   const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
   const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
   const float4 cf = a.coef[c];
-  const float4 bc = a.bcoef[c];  // (g = gamma*invstd, mdy, mdyx, -)
+  const BCoef bc = a.bcoef[c];
   const int rows = min(kR1, a.g.H1 - h0);
   const int nwin = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
   float v[5] = {0, 0, 0, 0, 0};
@@ -266,9 +278,7 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     for (int j = 0; j < 3; ++j) {
       if (j >= nw) continue;
       const float dy = (j == jm) ? dyv : 0.0f;
-      const float xh = (r[j] - cf.x) * cf.y;
-      const float dx = (dy - bc.y - xh * bc.z) * bc.x;
-      const float dz = r[j] > 0.0f ? dx : 0.0f;
+      const float dz = r[j] > 0.0f ? bn_dx(dy, r[j], cf, bc) : 0.0f;
       const float* x0 = xs + hl * a.g.W0 + w + j;
       v[0] = fmaf(dz, x0[0], v[0]);
       v[1] = fmaf(dz, x0[1], v[1]);
@@ -329,7 +339,7 @@ __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const
 // backward finalize: s1 = sum dy (-> dbeta), s2 = sum dy*xhat (-> dgamma); coefficients for dx
 __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, int nblk, int C, double count,
                                                              const float* gamma, const float4* coef, float* dgamma,
-                                                             float* dbeta, float4* bcoef) {
+                                                             float* dbeta, BCoef* bcoef) {
   const int c = blockIdx.x;
   double s1 = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) {
@@ -349,7 +359,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, 
     s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     dgamma[c] = (float)s2;
     dbeta[c] = (float)s1;
-    bcoef[c] = make_float4(gamma[c] * coef[c].y, (float)(s1 / count), (float)(s2 / count), 0.0f);
+    bcoef[c] = BCoef{(double)gamma[c] * (double)coef[c].y, s1 / count, s2 / count, 0.0};
   }
 }
 
@@ -374,7 +384,7 @@ struct PoolArgs {
   int flat_n;
   DropArgs drop;
   const float* dp;     // grad wrt pooled output (same layout as out)
-  const float4* bcoef;
+  const BCoef* bcoef;
   float* dz;           // NHWC
   float* part;
   int nblk;
@@ -446,7 +456,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a) {
   const int64_t total = (int64_t)a.B * a.H * a.W * a.C;
   const int c = threadIdx.x % a.C;
   const float4 cf = a.coef[c];
-  const float4 bc = a.bcoef[c];
+  const BCoef bc = a.bcoef[c];
   float v[1] = {0.0f};
   for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
     int64_t q = e / a.C;
@@ -462,9 +472,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a) {
       if (arg == h * a.W + w) dy = a.dp[pooled_index(a, b, ho, wo, c)];
     }
     const float rv = a.r[e];
-    const float xh = (rv - cf.x) * cf.y;
-    const float dx = (dy - bc.y - xh * bc.z) * bc.x;
-    const float dz = rv > 0.0f ? dx : 0.0f;
+    const float dz = rv > 0.0f ? bn_dx(dy, rv, cf, bc) : 0.0f;
     a.dz[e] = dz;
     v[0] += dz;
   }
@@ -937,7 +945,7 @@ struct Work {
   float* part;
   float* slab;
   float4* coef;   // 3 x 64
-  float4* bcoef;  // 3 x 64
+  BCoef* bcoef;   // 3 x 64
   uint8_t *mask1, *mask2;
   size_t bytes;
 };
@@ -986,7 +994,7 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
                                           (int64_t)kFc1MSplit * 128 * g.flat});
   w.slab = F(slab);
   w.coef = reinterpret_cast<float4*>(take(3 * 64 * sizeof(float4)));
-  w.bcoef = reinterpret_cast<float4*>(take(3 * 64 * sizeof(float4)));
+  w.bcoef = reinterpret_cast<BCoef*>(take(3 * 64 * sizeof(BCoef)));
   w.mask1 = reinterpret_cast<uint8_t*>(take((size_t)B * g.flat));
   w.mask2 = reinterpret_cast<uint8_t*>(take((size_t)B * 128));
   w.bytes = off;
@@ -1448,6 +1456,22 @@ int abd_smallcnn_flat_features(const abd_cnn* net) { return net ? net->g.flat : 
 size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch) {
   if (!net) return 0;
   return layout(net, batch, nullptr).bytes;
+}
+
+int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name) {
+  if (!net || !name) return -1;
+  char* base = reinterpret_cast<char*>(static_cast<uintptr_t>(4096));  // any non-null base: offsets only
+  const Work w = layout(net, batch, base);
+  const struct {
+    const char* n;
+    const void* p;
+  } tab[] = {{"p1", w.p1},     {"r2", w.r2},       {"p2", w.p2},     {"r3", w.r3},       {"p3d", w.p3d},
+             {"d2", w.d2},     {"logp", w.logp},   {"dz", w.dz},     {"dp3", w.dp3},     {"da", w.da},
+             {"dz3", w.dz3},   {"dp2", w.dp2},     {"dz2", w.dz2},   {"dp1", w.dp1},     {"coef", w.coef},
+             {"bcoef", w.bcoef}, {"mask1", w.mask1}, {"mask2", w.mask2}, {"rowinfo", w.rowinfo}};
+  for (const auto& t : tab)
+    if (strcmp(t.n, name) == 0) return (int64_t)(static_cast<const char*>(t.p) - base);
+  return -1;
 }
 
 int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspace, size_t workspace_bytes,

@@ -124,6 +124,9 @@ int64_t abd_smallcnn_param_count(const abd_cnn* net);
 int abd_smallcnn_param_offsets(const abd_cnn* net, int64_t* offsets /* 17 */);
 int abd_smallcnn_flat_features(const abd_cnn* net);
 size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch);
+/* Byte offset of a named activation buffer inside the workspace (tests / debugging):
+ * p1 r2 p2 r3 p3d d2 logp dz dp3 da dz3 dp2 dz2 dp1 coef bcoef mask1 mask2 rowinfo. */
+int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name);
 
 /* Device-side counters written by the train/eval launches (int64 / double):
  *   [0] sum of per-batch mean losses (double bits)  [1] samples  [2] correct

@@ -199,7 +199,8 @@ class SmallCNN:
         return loss, dz
 
     # backward ---------------------------------------------------------------
-    def backward(self, c, dz):
+    def backward(self, c, dz, record=None):
+        """Parameter gradients; ``record`` (dict) receives the intermediate gradients for layer-wise checks."""
         p = self.p
         g = {}
         g["fc2.weight"] = dz.T @ c["d2"]
@@ -210,11 +211,17 @@ class SmallCNN:
         g["fc1.bias"] = da.sum(axis=0)
         dflat = (da @ p["fc1.weight"]) * c["m1"]
         dh = dflat.reshape(c["p3shape"])
+        if record is not None:
+            record.update(da=da, dp3=dflat)
         for i in (3, 2, 1):
             dy = maxpool_backward(dh, c[f"arg{i}"], c[f"yshape{i}"])
             dr, g[f"bn{i}.weight"], g[f"bn{i}.bias"] = bn_backward(dy, c[f"bn{i}"], p[f"bn{i}.weight"])
             dzc = dr * (c[f"r{i}"] > 0)
             dx, g[f"conv{i}.weight"], g[f"conv{i}.bias"] = conv2x2_backward(c[f"in{i}"], p[f"conv{i}.weight"], dzc, need_dx=(i > 1))
+            if record is not None:
+                record[f"dz{i}"] = dzc
+                if i > 1:
+                    record[f"dp{i - 1}"] = dx
             dh = dx
         return g
 

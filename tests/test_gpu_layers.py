@@ -1,0 +1,83 @@
+"""GPU: layer-by-layer comparison of every smallcnn activation / gradient buffer with the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import abd_amd
+from abd_amd import models as M, training as T, _lib as L
+from golden_inputs import make_state, mfcc_like, patch
+from oracle import smallcnn as oc
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def ws_view(eng, ws, B, name, shape, dtype=torch.float32):
+    off = L.lib().abd_smallcnn_workspace_offset(eng.h, B, name.encode())
+    assert off >= 0, name
+    n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+    return ws[off:off + n].view(dtype).view(*shape).cpu().numpy()
+
+
+@pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 48)])
+def test_every_buffer_matches_oracle(shape):
+    assert torch.cuda.is_available()
+    abd_amd.load_library()
+    dev = torch.device("cuda", 0)
+    H, W, K, B = shape
+    g = oc.geometry(H, W)
+    lf = g["flat"]
+    st = make_state(H, W, K, lf, seed=3000 + H + W + K)
+    m = M.smallcnn(K, lf)
+    m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
+    m = m.to(dev).train()
+    r = np.random.Generator(np.random.PCG64(H * W + B))
+    x = mfcc_like(r, B, H, W)
+    y = r.integers(0, K, B).astype(np.int64)
+    ind = (r.random(B) < 0.2).astype(np.int64)
+    for i in np.nonzero(ind)[0]:
+        patch(x[i:i + 1])
+        y[i] = 2
+    xd = torch.tensor(x, device=dev)
+    eng = m.engine(xd)
+    mo = (torch.empty((B, lf), dtype=torch.uint8, device=dev), torch.empty((B, 128), dtype=torch.uint8, device=dev))
+    T.train_step(m, xd, torch.tensor(y, device=dev), torch.tensor(ind, device=dev), None, None, masks_out=mo, seed=7)
+    torch.cuda.synchronize()
+    ws = eng.workspace(B)
+    o = oc.SmallCNN(st)
+    m1, m2 = mo[0].cpu().numpy(), mo[1].cpu().numpy()
+    out, c = o.forward_train(x, m1, m2)
+    _, dz = o.ce_loss_and_grad(out, y)
+    rec = {}
+    o.backward(c, dz, record=rec)
+    nhwc = lambda a: np.transpose(a, (0, 2, 3, 1))  # noqa: E731
+    checks = [
+        ("p1", c["in2"], nhwc, (B, g["H1p"], g["W1p"], 64), 1e-5),
+        ("r2", c["r2"], nhwc, (B, g["H2"], g["W2"], 64), 1e-5),
+        ("p2", c["in3"], nhwc, (B, g["H2p"], g["W2p"], 64), 1e-5),
+        ("r3", c["r3"], nhwc, (B, g["H3"], g["W3"], 32), 1e-5),
+        ("p3d", c["d1"], None, (B, lf), 1e-5),
+        ("d2", c["d2"], None, (B, 128), 1e-5),
+        ("dz", dz, None, (B, K), 1e-5),
+        ("da", rec["da"], None, (B, 128), 1e-5),
+        ("dp3", rec["dp3"], None, (B, lf), 1e-5),
+        ("dz3", rec["dz3"], nhwc, (B, g["H3"], g["W3"], 32), 1e-5),
+        ("dp2", rec["dp2"], nhwc, (B, g["H2p"], g["W2p"], 64), 1e-5),
+        ("dz2", rec["dz2"], nhwc, (B, g["H2"], g["W2"], 64), 2e-5),
+        ("dp1", rec["dp1"], nhwc, (B, g["H1p"], g["W1p"], 64), 2e-5),
+    ]
+    report = {}
+    for name, ref, tf, shp, tol in checks:
+        got = ws_view(eng, ws, B, name, shp)
+        refv = tf(ref) if tf else ref
+        report[name] = nrel(got, refv)
+    print(shape, {k: f"{v:.1e}" for k, v in report.items()})
+    for name, ref, tf, shp, tol in checks:
+        assert report[name] < tol, (name, report[name])
