@@ -75,7 +75,7 @@ def conv2x2_backward(x, w, dout, need_dx=True):
     return dx, dw, db
 
 
-def maxpool(x, k, s, p):
+def maxpool(x, k, s, p, force_arg=None):
     """Returns (out, arg) with arg = flat index h*W+w of the first maximum in scan order."""
     B, C, H, W = x.shape
     kh, kw = k
@@ -90,6 +90,18 @@ def maxpool(x, k, s, p):
         for j in range(kw):
             cand[..., i * kw + j] = xp[:, :, i:i + sh * (Ho - 1) + 1:sh, j:j + sw * (Wo - 1) + 1:sw]
     a = np.argmax(cand, axis=-1)  # first occurrence == strict '>' scan
+    if force_arg is not None:
+        # replay another implementation's choice where it is admissible: the forced
+        # element must be within fp32 resolution of the window maximum
+        fa = (force_arg // W - (np.arange(Ho)[None, None, :, None] * sh - ph)) * kw + \
+             (force_arg % W - (np.arange(Wo)[None, None, None, :] * sw - pw))
+        top = np.take_along_axis(cand, a[..., None], axis=-1)[..., 0]
+        got = np.take_along_axis(cand, fa[..., None], axis=-1)[..., 0]
+        bad = top - got > 2e-6 * (np.abs(top) + 1e-3)
+        if bad.any():
+            raise AssertionError(f"{int(bad.sum())} forced pool choices are not near-ties")
+        maxpool.replayed = int((fa != a).sum())
+        a = fa
     out = np.take_along_axis(cand, a[..., None], axis=-1)[..., 0]
     hh = np.arange(Ho)[None, None, :, None] * sh - ph + a // kw
     ww = np.arange(Wo)[None, None, None, :] * sw - pw + a % kw
@@ -156,17 +168,35 @@ class SmallCNN:
         z = h @ p["fc2.weight"].T + p["fc2.bias"]
         return log_softmax(z)
 
-    def forward_train(self, x, mask1, mask2):
-        """mask1 (B, flat) and mask2 (B, 128) keep-masks in {0,1}."""
+    def forward_train(self, x, mask1, mask2, force=None):
+        """mask1 (B, flat) and mask2 (B, 128) keep-masks in {0,1}.
+
+        ``force`` = {layer: {"relu": bool (B,C,H,W), "arg": pool argmax}} replays another
+        implementation's discrete decisions, each checked to be a genuine fp32 near-tie
+        (c["replayed<i>"] counts how many differ from this oracle's own choice)."""
         p = self.p
         c = {"x": np.asarray(x, dtype=np.float64)}
         h = c["x"]
         for i in (1, 2, 3):
             c[f"in{i}"] = h
-            r = np.maximum(conv2x2(h, p[f"conv{i}.weight"], p[f"conv{i}.bias"]), 0.0)
+            z = conv2x2(h, p[f"conv{i}.weight"], p[f"conv{i}.bias"])
+            relu = z > 0
+            fi = (force or {}).get(i)
+            c[f"replayed{i}"] = 0
+            if fi is not None and "relu" in fi:
+                # admissible only where |z| is within fp32 resolution of zero
+                diff = fi["relu"] != relu
+                if np.any(np.abs(z[diff]) > 2e-6 * np.sqrt(np.mean(z * z))):
+                    raise AssertionError(f"layer {i}: forced ReLU decisions far from zero")
+                c[f"replayed{i}"] += int(diff.sum())
+                relu = fi["relu"]
+            r = np.where(relu, z, 0.0)
             c[f"r{i}"] = r
+            c[f"relu{i}"] = relu
             y, c[f"bn{i}"] = bn_train(r, p[f"bn{i}.weight"], p[f"bn{i}.bias"])
-            h, c[f"arg{i}"] = maxpool(y, *POOLS[i])
+            maxpool.replayed = 0
+            h, c[f"arg{i}"] = maxpool(y, *POOLS[i], force_arg=(fi or {}).get("arg"))
+            c[f"replayed{i}"] += maxpool.replayed
             c[f"yshape{i}"] = y.shape
         c["p3shape"] = h.shape
         flat = h.reshape(h.shape[0], -1)
@@ -216,7 +246,7 @@ class SmallCNN:
         for i in (3, 2, 1):
             dy = maxpool_backward(dh, c[f"arg{i}"], c[f"yshape{i}"])
             dr, g[f"bn{i}.weight"], g[f"bn{i}.bias"] = bn_backward(dy, c[f"bn{i}"], p[f"bn{i}.weight"])
-            dzc = dr * (c[f"r{i}"] > 0)
+            dzc = dr * c[f"relu{i}"]
             dx, g[f"conv{i}.weight"], g[f"conv{i}.bias"] = conv2x2_backward(c[f"in{i}"], p[f"conv{i}.weight"], dzc, need_dx=(i > 1))
             if record is not None:
                 record[f"dz{i}"] = dzc

@@ -9,15 +9,18 @@ from abd_amd import training as T
 from abd_amd import _lib as L
 from golden_inputs import EVAL_CFGS, TRAIN_CFGS, eval_inputs, make_state, train_inputs, unpack_mask, mfcc_like, patch
 from oracle import smallcnn as oc
+from gpu_replay import decisions
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-4  # north_star: 1e-4 relative fp32 tolerance
-# conv1's gradient is a 250k-term sum whose terms cancel ~250x (BatchNorm backward
-# subtracts the batch means).  A conv1 pre-activation within ~1e-7 of zero flips its
-# ReLU mask between ANY two fp32 summation orders (reference torch CPU included) and
-# the float64 oracle; at these batch sizes ~1 such element exists (measured:
-# 1 of 16M, |z| = 1.3e-7), worth up to ~1e-3 norm-relative on conv1 only.
-GRAD_TOL = {"conv1.weight": 2e-3, "conv1.bias": 2e-3}
+# A ReLU input within fp32 rounding of zero, or a max-pool window whose two largest
+# values are within fp32 rounding, is decided differently by ANY two fp32 summation
+# orders (the reference's torch CPU included) and the float64 oracle.  One such flip
+# moves a whole gradient element (~1/sqrt(N) of the norm) and later sums cancel
+# 200-5000x, so the large-batch tests replay the device's own decisions in the oracle
+# (tests/gpu_replay.py, each checked to be a genuine near-tie) and then hold every
+# continuous value to the fp32 tolerance.
+GRAD_TOL = {}
 
 
 @pytest.fixture(scope="module")
@@ -125,7 +128,8 @@ def test_train_step_gradients_vs_oracle(dev, shape):
     # dropout statistics: keep rates ~ 1-p
     assert abs(m1.mean() - 0.6) < 0.02 and abs(m2.mean() - 0.5) < 0.05
     o = oc.SmallCNN(st)
-    out, c = o.forward_train(x, m1, m2)
+    torch.cuda.synchronize()
+    out, c = o.forward_train(x, m1, m2, force=decisions(m._engine, B, x, st, g))
     np.testing.assert_allclose(lp.cpu().numpy(), out, rtol=RTOL, atol=RTOL * np.abs(out).max())
     loss, dz = o.ce_loss_and_grad(out, y)
     gref = o.backward(c, dz)
@@ -160,7 +164,8 @@ def test_autograd_path_matches_oracle(dev):
     assert out.requires_grad
     torch.nn.functional.cross_entropy(out, y).backward()
     o = oc.SmallCNN(st)
-    ref, c = o.forward_train(xn, mo[0].cpu().numpy(), mo[1].cpu().numpy())
+    ref, c = o.forward_train(xn, mo[0].cpu().numpy(), mo[1].cpu().numpy(),
+                             force=decisions(m._engine, B, xn, st, oc.geometry(H, W)))
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=RTOL, atol=RTOL * np.abs(ref).max())
     _, dz = o.ce_loss_and_grad(ref, yn)
     gref = o.backward(c, dz)
