@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a) {
 // ------------------------------------------------------------------ fp32 MFMA GEMMs
 // NT: C[m][n] = sum_t sum_c A_t(m)[c] * Bw[n][t*Cs + c]; A_t(m) is the NHWC channel row
 // of src at output position m shifted by tap t (zero outside the source grid).
-enum { EPI_STORE = 0, EPI_CONV = 1, EPI_FC1 = 2, EPI_DROPGRAD = 3 };
+enum { EPI_STORE = 0, EPI_CONV = 1, EPI_FC1 = 2, EPI_DROPGRAD = 3, EPI_PARTIAL = 4 };
 
 struct NTArgs {
   const float* src;
@@ -498,6 +498,7 @@ struct NTArgs {
   float* part;   // EPI_CONV stats partials [(j*N + n)*nblk + blk]
   int nblk;
   DropArgs drop;  // EPI_FC1 (dropout2 on relu(fc1)), EPI_DROPGRAD (dropout1 mask)
+  int ksplit;     // EPI_PARTIAL: K chunks split over blockIdx.z, raw sums to out[z][M][ldc]
 };
 
 constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
@@ -524,7 +525,10 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
     rw[i] = rem - rh[i] * a.Wo;
   }
   const int cpt = a.Cs / kKC;
-  const int nch = a.taps * cpt;
+  const int nch_all = a.taps * cpt;
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  const int ch_begin = (int)((int64_t)nch_all * blockIdx.z / ks);
+  const int nch = (int)((int64_t)nch_all * (blockIdx.z + 1) / ks);
   float4 ra[4], rbv[NJ];
   auto load = [&](int ch) {
     const int t = ch / cpt;
@@ -551,8 +555,8 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
 
-  load(0);
-  for (int ch = 0; ch < nch; ++ch) {
+  load(ch_begin);
+  for (int ch = ch_begin; ch < nch; ++ch) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float* d = As + ((tid >> 3) + 32 * i) * kLDA + 4 * q4;
@@ -598,7 +602,8 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
       const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= a.M || !cok) continue;
       float v = acc[j][r];
-      const int64_t oi = (int64_t)m * a.ldc + col;
+      int64_t oi = (int64_t)m * a.ldc + col;
+      if constexpr (EPI == EPI_PARTIAL) oi += (int64_t)blockIdx.z * a.M * a.ldc;
       if constexpr (EPI == EPI_CONV) {
         v = fmaxf(v + bias, 0.0f);
         st[j][0] += v;
@@ -858,31 +863,65 @@ __global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B
   }
 }
 
-// fc2 backward: dW2, db2 (thread per output, ordered sum over the batch) and
-// da = dd2 * scale2 * [d2 > 0]
+// fc2 data gradient through dropout2/ReLU: da = (dz . W2) * scale2 * [d2 > 0]
 __global__ void __launch_bounds__(kT) fc2_bwd_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
-                                                     float scale2, float* gw2, float* gb2, float* da) {
-  const int64_t nw = (int64_t)K * 128, nb = K, nd = (int64_t)B * 128;
-  const int64_t total = nw + nb + nd;
-  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    if (e < nw) {
-      const int k = (int)(e / 128), j = (int)(e % 128);
-      float s = 0.0f;
-      for (int b = 0; b < B; ++b) s = fmaf(dz[(int64_t)b * K + k], d2[(int64_t)b * 128 + j], s);
-      gw2[e] = s;
-    } else if (e < nw + nb) {
-      const int k = (int)(e - nw);
-      float s = 0.0f;
-      for (int b = 0; b < B; ++b) s += dz[(int64_t)b * K + k];
-      gb2[k] = s;
-    } else {
-      const int64_t f = e - nw - nb;
-      const int b = (int)(f / 128), j = (int)(f % 128);
-      float s = 0.0f;
-      for (int k = 0; k < K; ++k) s = fmaf(dz[(int64_t)b * K + k], w2[(int64_t)k * 128 + j], s);
-      da[f] = d2[f] > 0.0f ? s * scale2 : 0.0f;
-    }
+                                                     float scale2, float* da) {
+  const int64_t nd = (int64_t)B * 128;
+  for (int64_t f = blockIdx.x * (int64_t)kT + threadIdx.x; f < nd; f += (int64_t)gridDim.x * kT) {
+    const int b = (int)(f / 128), j = (int)(f % 128);
+    float s = 0.0f;
+    for (int k = 0; k < K; ++k) s = fmaf(dz[(int64_t)b * K + k], w2[(int64_t)k * 128 + j], s);
+    da[f] = d2[f] > 0.0f ? s * scale2 : 0.0f;
   }
+}
+
+// fc1: sum the split-K partials in order, + bias, ReLU, dropout2 -> d2
+__global__ void __launch_bounds__(kT) fc1_epilogue_kernel(const float* part, int ks, int B, const float* bias,
+                                                          DropArgs drop, float* d2) {
+  const int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x;
+  if (e >= (int64_t)B * 128) return;
+  float v = 0.0f;
+  for (int z = 0; z < ks; ++z) v += part[(int64_t)z * B * 128 + e];
+  d2[e] = drop_apply(drop, e, fmaxf(v + bias[e & 127], 0.0f));
+}
+
+// fc2 weight/bias gradient partials: grid (K, nsplit); 128 threads = hidden units
+__global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const float* d2, int B, int K, int rows,
+                                                       float* part) {
+  const int k = blockIdx.x, sp = blockIdx.y, j = threadIdx.x;
+  const int b0 = sp * rows, b1 = min(B, b0 + rows);
+  float s = 0.0f, sb = 0.0f;
+#pragma unroll 4
+  for (int b = b0; b < b1; ++b) {
+    const float g = dz[(int64_t)b * K + k];
+    s = fmaf(g, d2[(int64_t)b * 128 + j], s);
+    sb += g;
+  }
+  part[((int64_t)sp * K + k) * 129 + j] = s;
+  if (j == 0) part[((int64_t)sp * K + k) * 129 + 128] = sb;
+}
+
+__global__ void __launch_bounds__(kT) fc2_wgrad_reduce_kernel(const float* part, int nsplit, int K, float* gw,
+                                                              float* gb) {
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= K * 129) return;
+  float s = 0.0f;
+  for (int i = 0; i < nsplit; ++i) s += part[(int64_t)i * K * 129 + e];
+  const int k = e / 129, j = e % 129;
+  if (j < 128) gw[k * 128 + j] = s;
+  else gb[k] = s;
+}
+
+// stage 1 of the slab reduction: group sums (each group = up to 32 slabs, in order)
+__global__ void __launch_bounds__(kT) slab_group_kernel(const float* slab, int nslab, int64_t total, int gsize,
+                                                        float* part) {
+  const int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x;
+  if (e >= total) return;
+  const int g = blockIdx.y;
+  const int i0 = g * gsize, i1 = min(nslab, i0 + gsize);
+  float s = 0.0f;
+  for (int i = i0; i < i1; ++i) s += slab[(int64_t)i * total + e];
+  part[(int64_t)g * total + e] = s;
 }
 
 __global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, int cols, float* out) {
@@ -944,13 +983,15 @@ struct Work {
   float *w2f, *w2d, *w3f, *w3d, *f1t;
   float* part;
   float* slab;
+  float* slab2;   // group sums of slab (hierarchical reduce) / fc1 split-K partials
   float4* coef;   // 3 x 64
   BCoef* bcoef;   // 3 x 64
   uint8_t *mask1, *mask2;
   size_t bytes;
 };
 
-constexpr int kConv2Slabs = 256, kConv3Slabs = 256, kFc1MSplit = 8;
+constexpr int kConv2Slabs = 1024, kConv3Slabs = 1024, kFc1MSplit = 8, kFc1KSplit = 48, kFc2Split = 16;
+constexpr int kSlabGroup = 32;
 
 int64_t nblk_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + kR1 - 1) / kR1); }
 
@@ -993,6 +1034,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   const int64_t slab = std::max<int64_t>({(int64_t)kConv2Slabs * 64 * 256, (int64_t)kConv3Slabs * 32 * 256,
                                           (int64_t)kFc1MSplit * 128 * g.flat});
   w.slab = F(slab);
+  w.slab2 = F(std::max<int64_t>({(int64_t)(kConv2Slabs / kSlabGroup + 1) * 64 * 256, (int64_t)kFc1KSplit * B * 128,
+                                 (int64_t)kFc2Split * 64 * 129}));
   w.coef = reinterpret_cast<float4*>(take(3 * 64 * sizeof(float4)));
   w.bcoef = reinterpret_cast<BCoef*>(take(3 * 64 * sizeof(BCoef)));
   w.mask1 = reinterpret_cast<uint8_t*>(take((size_t)B * g.flat));
@@ -1100,10 +1143,27 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 
 template <int NB, int EPI>
 int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
-  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB);
-  abd::prof_begin(phase, s);
+  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
+  if (phase >= 0) abd::prof_begin(phase, s);
   gemm_nt_kernel<NB, EPI><<<grid, dim3(kT), 0, s>>>(a);
-  abd::prof_end(phase, s);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
+int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s) {
+  const int64_t total = (int64_t)N * Ktot;
+  const float* src = w.slab;
+  int n = nsl;
+  if (nsl > kSlabGroup) {
+    const int G = (nsl + kSlabGroup - 1) / kSlabGroup;
+    slab_group_kernel<<<dim3((unsigned)((total + kT - 1) / kT), (unsigned)G), kT, 0, s>>>(w.slab, nsl, total,
+                                                                                         kSlabGroup, w.slab2);
+    ABD_LAUNCH_CHECK();
+    src = w.slab2;
+    n = G;
+  }
+  slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out);
   ABD_LAUNCH_CHECK();
   return 0;
 }
@@ -1193,7 +1253,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     abd::prof_end(abd::PH_BN3_POOL, s);
     ABD_LAUNCH_CHECK();
   }
-  // ---- fc1 (MFMA) + relu + dropout2
+  // ---- fc1 (MFMA, split-K over the flat features) -> in-order sum + bias + relu + dropout2
   {
     NTArgs a{};
     a.src = w.p3d;
@@ -1204,11 +1264,15 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     a.Bw = P.p[P_F1W];
     a.ldb = g.flat;
     a.N = 128;
-    a.bias = P.p[P_F1B];
-    a.out = w.d2;
+    a.out = w.slab2;
     a.ldc = 128;
-    a.drop = drop2;
-    if (launch_nt<128, EPI_FC1>(a, s, abd::PH_FC1_FWD)) return -1;
+    a.ksplit = std::min(g.flat / kKC, kFc1KSplit);
+    abd::prof_begin(abd::PH_FC1_FWD, s);
+    if (launch_nt<128, EPI_PARTIAL>(a, s, -1)) return -1;
+    fc1_epilogue_kernel<<<(unsigned)((B * 128 + kT - 1) / kT), kT, 0, s>>>(w.slab2, a.ksplit, (int)B, P.p[P_F1B], drop2,
+                                                                           w.d2);
+    abd::prof_end(abd::PH_FC1_FWD, s);
+    ABD_LAUNCH_CHECK();
   }
   return 0;
 }
@@ -1249,8 +1313,13 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   const float s2 = 1.0f / (1.0f - kP2);
   // ---- fc2 + dropout2/relu
   abd::prof_begin(abd::PH_FC2_BWD, s);
-  fc2_bwd_kernel<<<grid_for((int64_t)g.K * 129 + B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, s2,
-                                                                          G[P_F2W], G[P_F2B], w.da);
+  {
+    const int rows = (int)((B + kFc2Split - 1) / kFc2Split);
+    fc2_wgrad_kernel<<<dim3((unsigned)g.K, (unsigned)kFc2Split), 128, 0, s>>>(w.dz, w.d2, (int)B, g.K, rows, w.slab2);
+    fc2_wgrad_reduce_kernel<<<(unsigned)((g.K * 129 + kT - 1) / kT), kT, 0, s>>>(w.slab2, kFc2Split, g.K, G[P_F2W],
+                                                                                G[P_F2B]);
+    fc2_bwd_kernel<<<grid_for(B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, s2, w.da);
+  }
   abd::prof_end(abd::PH_FC2_BWD, s);
   ABD_LAUNCH_CHECK();
   colsum_kernel<<<1, 128, 0, s>>>(w.da, (int)B, 128, G[P_F1B]);
@@ -1276,8 +1345,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     gemm_tn_kernel<128, 128><<<grid, kT, 0, s>>>(a);
     abd::prof_end(abd::PH_FC1_WGRAD, s);
     ABD_LAUNCH_CHECK();
-    slab_reduce_kernel<<<grid_for(128LL * g.flat), kT, 0, s>>>(w.slab, nsl, 128, g.flat, 0, G[P_F1W]);
-    ABD_LAUNCH_CHECK();
+    if (reduce_slabs(w, nsl, 128, g.flat, 0, G[P_F1W], s)) return -1;
   }
   // ---- fc1 data grad (NT against fc1.weight^T) * dropout1 mask
   {
@@ -1328,8 +1396,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     gemm_tn_kernel<32, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
     abd::prof_end(abd::PH_CONV3_WGRAD, s);
     ABD_LAUNCH_CHECK();
-    slab_reduce_kernel<<<grid_for(32 * 256), kT, 0, s>>>(w.slab, nsl, 32, 256, 64, G[P_C3W]);
-    ABD_LAUNCH_CHECK();
+    if (reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)) return -1;
   }
@@ -1361,8 +1428,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     gemm_tn_kernel<64, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
     abd::prof_end(abd::PH_CONV2_WGRAD, s);
     ABD_LAUNCH_CHECK();
-    slab_reduce_kernel<<<grid_for(64 * 256), kT, 0, s>>>(w.slab, nsl, 64, 256, 64, G[P_C2W]);
-    ABD_LAUNCH_CHECK();
+    if (reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)) return -1;
   }
