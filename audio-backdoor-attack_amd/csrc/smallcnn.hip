@@ -924,12 +924,16 @@ __global__ void __launch_bounds__(kT) slab_group_kernel(const float* slab, int n
   part[(int64_t)g * total + e] = s;
 }
 
+// column sums of a (rows, cols) matrix: one block per column, fixed reduction tree
 __global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, int cols, float* out) {
-  const int c = blockIdx.x * kT + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.0f;
-  for (int r = 0; r < rows; ++r) s += x[(int64_t)r * cols + c];
-  out[c] = s;
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < rows; r += kT) s += x[(int64_t)r * cols + c];
+  __shared__ double red[kT / kWave];
+  s = abd::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
 // ------------------------------------------------------------------ Adam (torch single-tensor semantics)
@@ -1319,10 +1323,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     fc2_wgrad_reduce_kernel<<<(unsigned)((g.K * 129 + kT - 1) / kT), kT, 0, s>>>(w.slab2, kFc2Split, g.K, G[P_F2W],
                                                                                 G[P_F2B]);
     fc2_bwd_kernel<<<grid_for(B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, s2, w.da);
+    colsum_kernel<<<128, kT, 0, s>>>(w.da, (int)B, 128, G[P_F1B]);
   }
   abd::prof_end(abd::PH_FC2_BWD, s);
-  ABD_LAUNCH_CHECK();
-  colsum_kernel<<<1, 128, 0, s>>>(w.da, (int)B, 128, G[P_F1B]);
   ABD_LAUNCH_CHECK();
   // ---- fc1 weight grad (TN: n = 128 units, k = flat features, reduce over batch)
   {

@@ -1,0 +1,73 @@
+"""Drop-in for the reference's prepare_dataset.py: MFCC on the MI355X + the dataset plumbing.
+
+Put ``audio-backdoor-attack_amd/dropin`` ahead of the reference checkout on
+``sys.path``; the attack scripts then import this module unchanged.
+"""
+import os
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+import _root  # noqa: F401
+from abd_amd.features import MFCC  # noqa: F401  (prepare_dataset.py:35-47)
+from abd_amd.io import read_wav, LABEL_SETS, train_test_split_35
+
+__all__ = ["MFCC", "BDDataset", "prepare_clean_dataset", "load_clean_data"]
+
+
+class BDDataset(Dataset):
+    """Dict samples {'mfcc', 'label', 'poison_indicator'} (prepare_dataset.py:13-33)."""
+
+    def __init__(self, mfcc_list, label_list, poison_index):
+        self.mfcc_list, self.label_list, self.poison_index = mfcc_list, label_list, poison_index
+
+    def __len__(self):
+        return len(self.mfcc_list)
+
+    def __getitem__(self, index):
+        return {"mfcc": self.mfcc_list[index], "label": self.label_list[index],
+                "poison_indicator": self.poison_index[index]}
+
+
+def prepare_clean_dataset(data_path, directory_name, labels, waveform_to_consider, n_mfcc, n_fft, hop_length,
+                          sr=16000, save=True):
+    """Load wavs (int16/32768), keep clips >= sr samples, batched MFCC on the device, 80/20 split (seed 35)."""
+    waves, labs = [], []
+    for li, label in enumerate(labels):
+        d = os.path.join(data_path, label)
+        for name in os.listdir(d):
+            if not name.endswith(".wav"):
+                continue
+            w, rate = read_wav(os.path.join(d, name))
+            if rate != sr:
+                raise NotImplementedError(f"{name}: resampling {rate}->{sr} Hz is not implemented yet "
+                                          "(SURVEY.md §8f item 4)")
+            if w.shape[0] >= waveform_to_consider:
+                waves.append(w[None, :waveform_to_consider])
+                labs.append(li)
+    waves = np.stack(waves).astype(np.float32)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    mf = MFCC(torch.tensor(waves, device=dev), sr, n_mfcc, n_fft, hop_length).transpose(2, 3).cpu().numpy()
+    tr, te = train_test_split_35(len(waves))
+    out = (waves[tr], waves[te], mf[tr], mf[te], np.array(labs)[tr], np.array(labs)[te])
+    if save:
+        path = directory_name + "/clean/"
+        os.makedirs(path, exist_ok=True)
+        for n, a in zip(("clean_train_wav", "clean_test_wav", "clean_train_mfcc", "clean_test_mfcc",
+                         "clean_train_label", "clean_test_label"), out):
+            np.save(path + n, a)
+    return out
+
+
+def load_clean_data(args, load=False):
+    """prepare_dataset.py:86-112: label set by --dataset, .npy cache under record/<result>/<dataset>/clean/."""
+    data_path, labels = LABEL_SETS[args.dataset]
+    directory_name = "record/" + args.result + "/" + args.dataset
+    if load:
+        path = directory_name + "/clean/"
+        return tuple(np.load(path + n + ".npy") for n in ("clean_train_wav", "clean_test_wav", "clean_train_mfcc",
+                                                          "clean_test_mfcc", "clean_train_label",
+                                                          "clean_test_label"))
+    return prepare_clean_dataset(data_path, directory_name, labels, args.sample_rate, args.n_mfcc, args.n_fft,
+                                 args.hop_length, sr=args.sample_rate, save=True)

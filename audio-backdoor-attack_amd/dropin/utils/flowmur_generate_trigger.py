@@ -1,0 +1,15 @@
+"""Drop-in for utils/flowmur_generate_trigger.py (the SNR mix runs in libabd)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _root  # noqa: F401,E402
+from abd_amd.triggers import deploy_trigger_to_waveform  # noqa: F401,E402
+
+
+def generate_trigger(benign_model, dataloader, trigger_length, path):
+    raise NotImplementedError("FlowMur trigger optimisation needs backward through MFCC (SURVEY.md §8f item 1)")
+
+
+def pretrain_model(train_data, train_label, test_data, test_label, path, num_classes):
+    raise NotImplementedError("use abd_amd.training.clean_train/clean_test with abd_amd.models.smallcnn(K, 224)")

@@ -1,0 +1,45 @@
+"""Data-parallel plumbing (one process per GPU, torch.distributed; RCCL on the GPU box, gloo on CPU).
+
+The path shards by utterance: every rank draws the same seeded epoch permutation and
+takes its contiguous slice of each global batch; the only exchange is ONE sum
+all-reduce of the flat fp32 gradient buffer per step (1.68 MB at 101x40),
+with the loss gradient pre-normalised by the GLOBAL batch inside the loss kernel
+(grad_scale = B_local / B_global), so the summed gradient is the global-batch mean.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_slice(pos: int, local_batch: int, rank: int, world: int):
+    """[start, stop) of this rank's rows in the global batch that begins at epoch offset ``pos``."""
+    s = pos + rank * local_batch
+    return s, s + local_batch
+
+
+def grad_scale(local_batch: int, global_batch: int) -> float:
+    return float(local_batch) / float(global_batch)
+
+
+def allreduce_grads(flat: torch.Tensor, group=None):
+    """Sum the flat gradient buffer over ranks (one collective per step)."""
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    return flat
+
+
+def reduce_metrics(m: torch.Tensor, group=None) -> torch.Tensor:
+    """Combine libabd metric words across ranks: counts summed, batch-mean loss averaged.
+
+    Word 0 holds a float64 (sum of per-batch mean losses); words 1-5 are int64 counts."""
+    out = m.clone()
+    loss = out[0:1].view(torch.float64).clone()
+    dist.all_reduce(loss, group=group)
+    world = dist.get_world_size(group)
+    loss /= world
+    cnt = out[1:6].clone()
+    dist.all_reduce(cnt, group=group)
+    out[1:5] = cnt[0:4]
+    out[5] = cnt[4] // world  # batches: every rank saw the same number of global batches
+    out[0:1] = loss.view(torch.int64)
+    return out

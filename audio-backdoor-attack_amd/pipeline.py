@@ -30,6 +30,7 @@ from . import _lib as L
 from . import features as F
 from .models import smallcnn
 from . import training as T
+from . import parallel_dp as DP
 
 TARGET_LABEL = 2  # badnets.py:115, ultrasonic.py:77, jingleback.py:72, flowmur.py:74
 
@@ -153,8 +154,7 @@ class ResidentTrainer:
         if self._epoch is None or self._pos + self.B * self.world > self.N:
             self.new_epoch()
         rows, lab, ind, pois, pos = self._epoch
-        s = self._pos + self.rank * self.B
-        e = s + self.B
+        s, e = DP.shard_slice(self._pos, self.B, self.rank, self.world)
         self._pos += self.B * self.world
         inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois[s:e],
                           position=pos[s:e] if pos is not None else None, snr_db=self.cfg.snr_db,
@@ -164,8 +164,8 @@ class ResidentTrainer:
             T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics)
         else:
             T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics, do_update=False,
-                         grad_scale=1.0 / self.world)
-            torch.distributed.all_reduce(self.model._engine.grads, group=self.pg)
+                         grad_scale=DP.grad_scale(self.B, self.B * self.world))
+            DP.allreduce_grads(self.model._engine.grads, self.pg)
             T.apply_adam(self.model, self.adam, self.dev)
 
     def run_epoch(self):
@@ -178,11 +178,7 @@ class ResidentTrainer:
     def read_metrics(self, reduce=True):
         m = self.metrics.clone()
         if self.world > 1 and reduce:
-            loss = m[0:1].view(torch.float64).clone()
-            torch.distributed.all_reduce(loss, group=self.pg)
-            torch.distributed.all_reduce(m[1:6], group=self.pg)
-            loss /= self.world
-            m[0:1] = loss.view(torch.int64)
+            m = DP.reduce_metrics(m, self.pg)
         loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
         return {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
                 "asr": 100.0 * ah / max(pt, 1), "samples": total, "poisoned": pt}

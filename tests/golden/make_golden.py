@@ -132,6 +132,15 @@ def gen_train(out):
             out[f"train_{name}_expavgsq_{pid[p]}"] = digest(st["exp_avg_sq"].numpy(), 14)
 
 
+def gen_init(out):
+    """Reference smallcnn default init under a fixed torch seed (the drop-in must match it)."""
+    for K, lf in ((10, 3072), (35, 3072), (10, 224)):
+        torch.manual_seed(123)
+        m = ref_models.smallcnn(K, lf)
+        for k, v in m.state_dict().items():
+            out[f"init_{K}_{lf}_{k}"] = digest(v.numpy(), 15)
+
+
 def gen_badnets(out):
     out["badnet_trigger_101x40"] = ref_bt.generate_trigger(40, 101, 5, save=False)
     out["badnet_trigger_32x13_s3_d1"] = ref_bt.generate_trigger(13, 32, 3, 1, 2, save=False)
@@ -157,6 +166,7 @@ def main():
     out = {}
     gen_eval(out)
     gen_train(out)
+    gen_init(out)
     gen_badnets(out)
     np.savez_compressed(os.path.join(HERE, "golden_ref.npz"), **out)
     wavs = {}
