@@ -20,8 +20,10 @@
 #include "abd_common.h"
 #include "prof.h"
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -32,7 +34,7 @@ constexpr int kMaxComplexPerBlock = 6144;  // ppb * M  (LDS: 2 * 8 B * this = 96
 constexpr int kTT = 8;                     // frames per db_dct block
 
 struct MfccDev {
-  int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass;
+  int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
   int64_t L;
   float top_db;
   int radix[16], ns[16];
@@ -410,6 +412,294 @@ __global__ void __launch_bounds__(kThreads) pydub_overlay_kernel(const int16_t* 
   }
 }
 
+
+// =====================================================================================
+// Specialised STFT+mel kernel for the attack geometries (compile-time radix plans).
+//   n_fft 1103 (ultrasonic, Bluestein M = 2304 = 16*16*9), 2048 = 16*16*8 (flowmur, daba),
+//   400 = 16*25 (badnets, jingleback).
+// vs the generic kernel: radix-16/25/9/8 butterflies in registers (2-3 LDS passes instead of
+// 4-6), divisions by compile-time constants, twiddle table in LDS (persistent blocks load it
+// once), in-place passes (read -> barrier -> write), Bluestein's pointwise spectrum product
+// fused into the second FFT's first pass, mel projection straight from the packed spectrum.
+// =====================================================================================
+constexpr double cx_pi = 3.14159265358979323846264338327950288;
+constexpr double cx_sin_small(double x) {
+  double x2 = x * x, term = x, sum = x;
+  for (int i = 1; i < 14; ++i) {
+    term *= -x2 / ((2.0 * i) * (2.0 * i + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double cx_cos_small(double x) {
+  double x2 = x * x, term = 1.0, sum = 1.0;
+  for (int i = 1; i < 14; ++i) {
+    term *= -x2 / ((2.0 * i - 1.0) * (2.0 * i));
+    sum += term;
+  }
+  return sum;
+}
+// (cos, sin)(2 pi m / N) by octant reduction (exact at octant boundaries)
+constexpr double cx_trig2pi(int m, int N, bool want_sin) {
+  m %= N;
+  if (m < 0) m += N;
+  const int o = (8 * m) / N;
+  const double a = 2.0 * cx_pi * m / N - o * (cx_pi / 4.0);
+  const double ca = cx_cos_small(a), sa = cx_sin_small(a);
+  const double r = 0.70710678118654752440084436210485;
+  const double cb[8] = {1, r, 0, -r, -1, -r, 0, r}, sb[8] = {0, r, 1, r, 0, -r, -1, -r};
+  return want_sin ? sb[o] * ca + cb[o] * sa : cb[o] * ca - sb[o] * sa;
+}
+template <int N>
+struct TwTab {
+  float c[N];
+  float s[N];  // exp(-2 pi i m / N) = (c, s)
+  constexpr TwTab() : c(), s() {
+    for (int m = 0; m < N; ++m) {
+      c[m] = (float)cx_trig2pi(m, N, false);
+      s[m] = (float)-cx_trig2pi(m, N, true);
+    }
+  }
+};
+template <int N>
+__device__ constexpr TwTab<N> kTw{};
+
+template <int R>
+__device__ __forceinline__ void dftn(float2* v);
+template <>
+__device__ __forceinline__ void dftn<2>(float2* v) { dft<2>(v); }
+template <>
+__device__ __forceinline__ void dftn<3>(float2* v) { dft<3>(v); }
+template <>
+__device__ __forceinline__ void dftn<4>(float2* v) { dft<4>(v); }
+template <>
+__device__ __forceinline__ void dftn<5>(float2* v) { dft<5>(v); }
+
+// Cooley-Tukey N = N1*N2 in registers, natural-order in and out.
+template <int N1, int N2>
+__device__ __forceinline__ void dft_comp(float2* v) {
+  constexpr int N = N1 * N2;
+  float2 t[N1];
+#pragma unroll
+  for (int n2 = 0; n2 < N2; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < N1; ++n1) t[n1] = v[N2 * n1 + n2];
+    dftn<N1>(t);
+#pragma unroll
+    for (int k1 = 0; k1 < N1; ++k1) {
+      const int e = (n2 * k1) % N;
+      v[N2 * k1 + n2] = (e == 0) ? t[k1] : cmul(t[k1], make_float2(kTw<N>.c[e], kTw<N>.s[e]));
+    }
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < N1; ++k1) dftn<N2>(v + N2 * k1);
+  float2 o[N];
+#pragma unroll
+  for (int k1 = 0; k1 < N1; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < N2; ++k2) o[k1 + N1 * k2] = v[N2 * k1 + k2];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = o[i];
+}
+template <>
+__device__ __forceinline__ void dftn<8>(float2* v) { dft_comp<2, 4>(v); }
+template <>
+__device__ __forceinline__ void dftn<9>(float2* v) { dft_comp<3, 3>(v); }
+template <>
+__device__ __forceinline__ void dftn<16>(float2* v) { dft_comp<4, 4>(v); }
+template <>
+__device__ __forceinline__ void dftn<25>(float2* v) { dft_comp<5, 5>(v); }
+
+// One in-place Stockham pass over PP FFTs of length M: every thread reads all its
+// butterflies into registers, barrier, writes them back in Stockham order, barrier.
+template <int M, int R, int NS, int PP, bool VMUL>
+__device__ __forceinline__ void pass_inplace(float2* __restrict__ buf, const float2* __restrict__ tw,
+                                             const float2* __restrict__ vhat) {
+  constexpr int MR = M / R;
+  constexpr int NB = PP * MR;
+  constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
+  constexpr int TSTEP = M / (NS * R);
+  float2 v[ROUNDS][R];
+#pragma unroll
+  for (int rd = 0; rd < ROUNDS; ++rd) {
+    const int g = threadIdx.x + rd * kThreads;
+    if (ROUNDS * kThreads == NB || g < NB) {
+      const int f = g / MR;
+      const int j = g - f * MR;
+      const float2* src = buf + f * M;
+      const int k = (NS == 1) ? 0 : j % NS;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float2 a = src[j + r * MR];
+        if constexpr (VMUL) a = cmul(make_float2(a.x, -a.y), vhat[j + r * MR]);
+        if (NS > 1 && r > 0) a = cmul(a, tw[k * r * TSTEP]);
+        v[rd][r] = a;
+      }
+      dftn<R>(v[rd]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int rd = 0; rd < ROUNDS; ++rd) {
+    const int g = threadIdx.x + rd * kThreads;
+    if (ROUNDS * kThreads == NB || g < NB) {
+      const int f = g / MR;
+      const int j = g - f * MR;
+      const int k = (NS == 1) ? 0 : j % NS;
+      float2* dst = buf + f * M + (j - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[r * NS] = v[rd][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int M, int R0, int R1, int R2, int PP, bool VMUL>
+__device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const float2* vhat) {
+  static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
+  pass_inplace<M, R0, 1, PP, VMUL>(buf, tw, vhat);
+  pass_inplace<M, R1, R0, PP, false>(buf, tw, vhat);
+  if constexpr (R2 > 1) pass_inplace<M, R2, R0 * R1, PP, false>(buf, tw, vhat);
+}
+
+template <int M, int R0, int R1, int R2, int PP, bool BLUE>
+__global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
+                                                                 int64_t row_stride,
+                                                                 const int32_t* __restrict__ rows, int64_t batch,
+                                                                 InjDev inj, const float* __restrict__ rowscale,
+                                                                 float* __restrict__ ws_db,
+                                                                 float* __restrict__ ws_max) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  float2* tw = lds;
+  float2* buf = lds + M;
+  __shared__ float red[kThreads / kWave];
+  for (int i = threadIdx.x; i < M; i += kThreads) tw[i] = p.tw[i];
+  const int chunks = p.chunks;
+  const int64_t n_items = batch * chunks;
+  const int64_t per = (n_items + gridDim.x - 1) / gridDim.x;
+  const int64_t i0 = blockIdx.x * per, i1 = min(n_items, i0 + per);
+  const int P = (p.T + 1) / 2;
+  for (int64_t item = i0; item < i1; ++item) {
+    const int64_t u = item / chunks;
+    const int c = (int)(item - u * chunks);
+    const int64_t row = rows ? rows[u] : u;
+    const float* x = wave + row * row_stride;
+    const bool pois = row_poisoned(inj, u);
+    const int pos = (inj.position != nullptr) ? inj.position[u] : 0;
+    const float rs = (rowscale != nullptr) ? rowscale[u] : 0.0f;
+    const int p0 = c * PP;
+    const int np = min(PP, P - p0);
+    __syncthreads();  // previous item fully consumed (and twiddles staged on the first pass)
+    for (int idx = threadIdx.x; idx < PP * M; idx += kThreads) {
+      const int f = idx / M;
+      const int n = idx - f * M;
+      float2 z = make_float2(0.0f, 0.0f);
+      if (f < np && n < p.N) {
+        const int t0 = 2 * (p0 + f), t1 = t0 + 1;
+        const float a = padded_sample(x, (int64_t)t0 * p.hop + n, p, inj, pois, pos, rs);
+        const float b = (t1 < p.T) ? padded_sample(x, (int64_t)t1 * p.hop + n, p, inj, pois, pos, rs) : 0.0f;
+        if constexpr (BLUE) {
+          z = cmul(make_float2(a, b), p.chirp_in[n]);
+        } else {
+          const float w = p.window[n];
+          z = make_float2(a * w, b * w);
+        }
+      }
+      buf[idx] = z;
+    }
+    __syncthreads();
+    fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+    if constexpr (BLUE) {
+      fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
+      // X[k] = conj(w[k] R[k]) / M for k < N
+      for (int idx = threadIdx.x; idx < np * p.N; idx += kThreads) {
+        const int f = idx / p.N;
+        const int k = idx - f * p.N;
+        const float2 r = cmul(p.chirp_out[k], buf[f * M + k]);
+        buf[f * M + k] = make_float2(r.x, -r.y);
+      }
+      __syncthreads();
+    }
+    // two real spectra from the packed one -> power -> mel -> dB
+    float lmax = -INFINITY;
+    for (int idx = threadIdx.x; idx < np * p.n_mels; idx += kThreads) {
+      const int f = idx / p.n_mels;
+      const int m = idx - f * p.n_mels;
+      const float2* Z = buf + f * M;
+      const int st = p.mel_start[m], cnt = p.mel_count[m];
+      const float* w = p.mel_w + p.mel_off[m];
+      float acc_a = 0.0f, acc_b = 0.0f;
+      for (int i = 0; i < cnt; ++i) {
+        const int k = st + i;
+        const int kn = (k == 0) ? 0 : p.N - k;
+        const float2 P1 = Z[k], Q = Z[kn];
+        const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
+        const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
+        acc_a = fmaf(ar * ar + ai * ai, w[i], acc_a);
+        acc_b = fmaf(br * br + bi * bi, w[i], acc_b);
+      }
+      const int ta = 2 * (p0 + f);
+      const float da = 10.0f * log10f(fmaxf(acc_a, 1e-10f));
+      ws_db[((int64_t)u * p.T + ta) * p.n_mels + m] = da;
+      lmax = fmaxf(lmax, da);
+      if (ta + 1 < p.T) {
+        const float db = 10.0f * log10f(fmaxf(acc_b, 1e-10f));
+        ws_db[((int64_t)u * p.T + ta + 1) * p.n_mels + m] = db;
+        lmax = fmaxf(lmax, db);
+      }
+    }
+    lmax = abd::wave_max(lmax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float mm = red[0];
+      for (int i = 1; i < kThreads / kWave; ++i) mm = fmaxf(mm, red[i]);
+      ws_max[u * chunks + c] = mm;
+    }
+  }
+}
+
+struct FastPlan {
+  int M, N, bluestein, pp;
+};
+constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1}, {2048, 2048, 0, 4}, {400, 400, 0, 13}};
+
+const FastPlan* find_fast(int M, int N, int blue) {
+  for (const auto& f : kFastPlans)
+    if (f.M == M && f.N == N && f.bluestein == blue) return &f;
+  return nullptr;
+}
+
+template <int M, int R0, int R1, int R2, int PP, bool BLUE>
+int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
+                const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, hipStream_t s) {
+  const size_t lds = (size_t)(PP + 1) * M * sizeof(float2);
+  static bool attr_set = false;
+  if (!attr_set) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&stft_mel_fast_kernel<M, R0, R1, R2, PP, BLUE>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = true;
+  }
+  const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 64)));
+  const int64_t items = batch * d.chunks;
+  const int grid = (int)std::min<int64_t>(items, 256LL * per_cu);
+  stft_mel_fast_kernel<M, R0, R1, R2, PP, BLUE><<<grid, kThreads, lds, s>>>(d, wave, row_stride, rows, batch, ij,
+                                                                            rowscale, ws_db, ws_max);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
+int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
+                  const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, hipStream_t s) {
+  if (d.M == 2304 && d.bluestein)
+    return launch_fast<2304, 16, 16, 9, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
+  if (d.M == 2048 && !d.bluestein)
+    return launch_fast<2048, 16, 16, 8, 4, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
+  if (d.M == 400 && !d.bluestein)
+    return launch_fast<400, 16, 25, 1, 13, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
+  return -1;
+}
+
 // ------------------------------------------------------------------ host side
 bool smooth235(int n) {
   for (int f : {2, 3, 5})
@@ -511,10 +801,18 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.T = (int)(1 + (length + 2 * (N / 2) - N) / hop_length);
   d.top_db = top_db;
   const int P = (d.T + 1) / 2;
-  int ppb_max = std::max(1, kMaxComplexPerBlock / M);
-  int chunks = (P + ppb_max - 1) / ppb_max;
-  d.ppb = (P + chunks - 1) / chunks;
-  d.chunks = (P + d.ppb - 1) / d.ppb;
+  const FastPlan* fp = find_fast(M, N, blue ? 1 : 0);
+  if (fp != nullptr && getenv("ABD_GENERIC_FFT") == nullptr) {
+    d.ppb = fp->pp;  // fixed pairs per work item (compile-time in the fast kernel)
+    d.chunks = (P + d.ppb - 1) / d.ppb;
+    d.fast = 1;
+  } else {
+    int ppb_max = std::max(1, kMaxComplexPerBlock / M);
+    int chunks = (P + ppb_max - 1) / ppb_max;
+    d.ppb = (P + chunks - 1) / chunks;
+    d.chunks = (P + d.ppb - 1) / d.ppb;
+    d.fast = 0;
+  }
   auto rad = factorize(M);
   d.n_pass = (int)rad.size();
   int Ns = 1;
@@ -775,8 +1073,12 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   ABD_CHECK(nblk < (1LL << 31), ABD_E_INVALID, "batch too large");
   const size_t lds = 2 * (size_t)d.ppb * d.M * sizeof(float2);
   abd::prof_begin(abd::PH_STFT_MEL, s);
-  stft_mel_kernel<<<dim3((unsigned)nblk), dim3(kThreads), lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale,
-                                                                  ws_db, ws_max);
+  if (d.fast) {
+    if (dispatch_fast(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s) != 0) return -1;
+  } else {
+    stft_mel_kernel<<<dim3((unsigned)nblk), dim3(kThreads), lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale,
+                                                                    ws_db, ws_max);
+  }
   abd::prof_end(abd::PH_STFT_MEL, s);
   ABD_LAUNCH_CHECK();
   abd::prof_begin(abd::PH_DB_DCT, s);

@@ -150,3 +150,21 @@ def test_pydub_overlay_kernel(dev):
                                           L.stream_ptr()), "overlay")
     exp = np.stack([otr.pydub_overlay(host[i], otr.pydub_gain(trig[i], float(gains[i]))) for i in range(4)])
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("cfg", CFGS[:4], ids=lambda c: f"generic-{c[0]}-{c[2]}")
+def test_generic_fft_kernel_matches_oracle(dev, cfg, monkeypatch):
+    """The generic runtime-plan kernel (fallback for n_fft without a specialised plan)."""
+    monkeypatch.setenv("ABD_GENERIC_FFT", "1")
+    F._PLANS.clear()
+    try:
+        test_mfcc_matches_oracle(dev, cfg)
+    finally:
+        monkeypatch.delenv("ABD_GENERIC_FFT")
+        F._PLANS.clear()
+
+
+def test_plan_description(dev):
+    c = F.MfccConfig.torchaudio(44100, 40, 1103, 441, 44100)
+    d = F.get_plan(c, dev).describe()
+    assert d["bluestein"] and d["fft_size"] == 2304 and d["n_frames"] == 100
