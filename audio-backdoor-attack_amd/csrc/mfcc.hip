@@ -35,6 +35,7 @@ constexpr int kTT = 8;                     // frames per db_dct block
 
 struct MfccDev {
   int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
+  int ablate;  // diagnostics only (ABD_STFT_ABLATE): 1 skip sample loads, 2 skip FFTs, 4 skip mel
   int64_t L;
   float top_db;
   int radix[16], ns[16];
@@ -596,8 +597,9 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
       float2 z = make_float2(0.0f, 0.0f);
       if (f < np && n < p.N) {
         const int t0 = 2 * (p0 + f), t1 = t0 + 1;
-        const float a = padded_sample(x, (int64_t)t0 * p.hop + n, p, inj, pois, pos, rs);
-        const float b = (t1 < p.T) ? padded_sample(x, (int64_t)t1 * p.hop + n, p, inj, pois, pos, rs) : 0.0f;
+        const bool skip = p.ablate & 1;
+        const float a = skip ? (float)n : padded_sample(x, (int64_t)t0 * p.hop + n, p, inj, pois, pos, rs);
+        const float b = skip ? (float)t1 : ((t1 < p.T) ? padded_sample(x, (int64_t)t1 * p.hop + n, p, inj, pois, pos, rs) : 0.0f);
         if constexpr (BLUE) {
           z = cmul(make_float2(a, b), p.chirp_in[n]);
         } else {
@@ -608,9 +610,9 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
       buf[idx] = z;
     }
     __syncthreads();
-    fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+    if (!(p.ablate & 2)) fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
     if constexpr (BLUE) {
-      fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
+      if (!(p.ablate & 2)) fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
       // X[k] = conj(w[k] R[k]) / M for k < N
       for (int idx = threadIdx.x; idx < np * p.N; idx += kThreads) {
         const int f = idx / p.N;
@@ -622,7 +624,7 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
     }
     // two real spectra from the packed one -> power -> mel -> dB
     float lmax = -INFINITY;
-    for (int idx = threadIdx.x; idx < np * p.n_mels; idx += kThreads) {
+    for (int idx = threadIdx.x; idx < ((p.ablate & 4) ? 0 : np * p.n_mels); idx += kThreads) {
       const int f = idx / p.n_mels;
       const int m = idx - f * p.n_mels;
       const float2* Z = buf + f * M;
@@ -806,6 +808,8 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     d.ppb = fp->pp;  // fixed pairs per work item (compile-time in the fast kernel)
     d.chunks = (P + d.ppb - 1) / d.ppb;
     d.fast = 1;
+    const char* ab = getenv("ABD_STFT_ABLATE");
+    d.ablate = ab ? atoi(ab) : 0;
   } else {
     int ppb_max = std::max(1, kMaxComplexPerBlock / M);
     int chunks = (P + ppb_max - 1) / ppb_max;
