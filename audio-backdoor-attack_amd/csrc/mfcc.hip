@@ -32,6 +32,8 @@ constexpr int kThreads = 256;
 using abd::kWave;
 constexpr int kMaxComplexPerBlock = 6144;  // ppb * M  (LDS: 2 * 8 B * this = 96 KiB max)
 constexpr int kTT = 8;                     // frames per db_dct block
+constexpr int kQueues = 8;                 // fast-kernel item queues (one per XCD)
+constexpr int kQueueStride = 64;           // unsigned words between queue counters (256 B)
 
 struct MfccDev {
   int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
@@ -49,6 +51,11 @@ struct MfccDev {
   const int* mel_off;
   const float* mel_w;
   const float* dct;
+  // fast (specialised) kernel tables
+  const float2* ftw;      // [W_{R0 R1}^e] ++ [W_M^k], e, k < R0 R1
+  const int4* mel2_meta;  // per half-filter slot 2m+h: (first bin, count, weight offset, 0)
+  const float* mel2_w;    // compact slot weights
+  int mel2_total, mel2_hp;  // #weights, max slot count rounded up to 8
 };
 
 struct InjDev {
@@ -511,29 +518,64 @@ __device__ __forceinline__ void dftn<16>(float2* v) { dft_comp<4, 4>(v); }
 template <>
 __device__ __forceinline__ void dftn<25>(float2* v) { dft_comp<5, 5>(v); }
 
-// One in-place Stockham pass over PP FFTs of length M: every thread reads all its
-// butterflies into registers, barrier, writes them back in Stockham order, barrier.
-template <int M, int R, int NS, int PP, bool VMUL>
-__device__ __forceinline__ void pass_inplace(float2* __restrict__ buf, const float2* __restrict__ tw,
-                                             const float2* __restrict__ vhat) {
+// threadIdx.x behind an opaque move.  The persistent item loop would otherwise hoist every
+// thread-invariant LDS/global address of all passes out of the loop and keep them live
+// (~150 extra VGPRs, occupancy 1-2); recomputing them per use costs a few VALU ops.
+__device__ __forceinline__ int ltid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  __builtin_assume(t >= 0 && t < kThreads);
+  return t;
+}
+
+// LDS layout of the fast kernel's FFT buffers: element i lives at i + (i >> 4) (one pad
+// slot per 16 complex).  The first Stockham pass writes j*R + r across lanes (stride 16
+// complex = 128 B: a 16-way conflict on ds_write_b64's 16-lane groups); padded, those
+// writes hit distinct banks, and offsets that are multiples of 16 stay affine
+// (pidx(i + 16q) = pidx(i) + 17q) so the passes keep base + immediate addressing.
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+// w[r] = w1^r for r < R by repeated squaring / one multiply (<= 4 roundings deep).
+template <int R>
+__device__ __forceinline__ void tw_powers(float2 w1, float2* w) {
+  w[1] = w1;
+#pragma unroll
+  for (int r = 2; r < R; ++r) w[r] = (r % 2 == 0) ? cmul(w[r / 2], w[r / 2]) : cmul(w[r - 1], w1);
+}
+
+// One in-place Stockham pass over PP FFTs of length M: every thread reads its butterflies
+// into registers, barrier, writes them back in Stockham order, barrier.
+//   TWK 0: first pass (no twiddles)
+//   TWK 1: tw = W_{NS*R}^e table, factor W_{NS*R}^{k r} read directly (k < NS, r < R)
+//   TWK 2: tw = W_M^k table (k < NS, NS*R == M), factor (W_M^k)^r by tw_powers
+//   VMUL : fold Bluestein's pointwise product conj(a) * vhat into the loads
+template <int M, int R, int NS, int PP, int TWK, bool VMUL>
+__device__ __forceinline__ void spass(float2* __restrict__ buf, const float2* __restrict__ tw,
+                                      const float2* __restrict__ vhat) {
   constexpr int MR = M / R;
   constexpr int NB = PP * MR;
   constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
-  constexpr int TSTEP = M / (NS * R);
   float2 v[ROUNDS][R];
 #pragma unroll
   for (int rd = 0; rd < ROUNDS; ++rd) {
-    const int g = threadIdx.x + rd * kThreads;
+    const int g = ltid() + rd * kThreads;
     if (ROUNDS * kThreads == NB || g < NB) {
       const int f = g / MR;
       const int j = g - f * MR;
-      const float2* src = buf + f * M;
+      const int rb = f * M + j;
+      const int prb = pidx(rb);
       const int k = (NS == 1) ? 0 : j % NS;
+      float2 w[R];
+      if constexpr (TWK == 2) tw_powers<R>(tw[k], w);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        float2 a = src[j + r * MR];
+        // MR % 16 == 0: pidx(rb + r MR) = pidx(rb) + r (MR + MR/16) -> base + immediate
+        float2 a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
         if constexpr (VMUL) a = cmul(make_float2(a.x, -a.y), vhat[j + r * MR]);
-        if (NS > 1 && r > 0) a = cmul(a, tw[k * r * TSTEP]);
+        if constexpr (TWK == 1) {
+          if (r > 0) a = cmul(a, tw[k * r]);
+        } else if constexpr (TWK == 2) {
+          if (r > 0) a = cmul(a, w[r]);
+        }
         v[rd][r] = a;
       }
       dftn<R>(v[rd]);
@@ -542,45 +584,199 @@ __device__ __forceinline__ void pass_inplace(float2* __restrict__ buf, const flo
   __syncthreads();
 #pragma unroll
   for (int rd = 0; rd < ROUNDS; ++rd) {
-    const int g = threadIdx.x + rd * kThreads;
+    const int g = ltid() + rd * kThreads;
     if (ROUNDS * kThreads == NB || g < NB) {
       const int f = g / MR;
       const int j = g - f * MR;
       const int k = (NS == 1) ? 0 : j % NS;
-      float2* dst = buf + f * M + (j - k) * R + k;
+      const int dst = f * M + (j - k) * R + k;
+      const int pd = pidx(dst);
+      // first pass: dst = j*16, r < 16; later passes: NS % 16 == 0 -> affine as above
+      constexpr bool AFF = (NS == 1) ? (R == 16) : (NS % 16 == 0);
 #pragma unroll
-      for (int r = 0; r < R; ++r) dst[r * NS] = v[rd][r];
+      for (int r = 0; r < R; ++r)
+        buf[AFF ? pd + r * (NS + NS / 16) : pidx(dst + r * NS)] = v[rd][r];
     }
   }
   __syncthreads();
 }
 
+// tw: [W_{R0 R1}^e, e < R0 R1] ++ [W_M^k, k < R0 R1]
 template <int M, int R0, int R1, int R2, int PP, bool VMUL>
 __device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const float2* vhat) {
   static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
-  pass_inplace<M, R0, 1, PP, VMUL>(buf, tw, vhat);
-  pass_inplace<M, R1, R0, PP, false>(buf, tw, vhat);
-  if constexpr (R2 > 1) pass_inplace<M, R2, R0 * R1, PP, false>(buf, tw, vhat);
+  spass<M, R0, 1, PP, 0, VMUL>(buf, nullptr, vhat);
+  spass<M, R1, R0, PP, 1, false>(buf, tw, nullptr);
+  if constexpr (R2 > 1) spass<M, R2, R0 * R1, PP, 2, false>(buf, tw + R0 * R1, nullptr);
 }
 
-template <int M, int R0, int R1, int R2, int PP, bool BLUE>
+// Injected sample at signal index s (already clamped into [0, L)); branch-free so the
+// gather below can keep every load of a group in flight.  Same arithmetic as inj_sample.
+template <int MODE>
+__device__ __forceinline__ float fsample(const float* __restrict__ x, const InjDev& inj, int s, int pos, float rs) {
+  const float v = x[s];
+  if constexpr (MODE == ABD_INJECT_ADD) {
+    const int tl = (int)inj.trig_len;
+    const float t = inj.trig[min(s, tl - 1)];
+    return (s < tl) ? v + t : v;
+  } else if constexpr (MODE == ABD_INJECT_SNR_WINDOW || MODE == ABD_INJECT_HALF_MIX || MODE == ABD_INJECT_DEPLOY) {
+    const int tl = (int)inj.trig_len;
+    const int o = s - pos;
+    const bool in = o >= 0 && o < tl;
+    const float t = inj.trig[min(max(o, 0), tl - 1)];
+    if constexpr (MODE == ABD_INJECT_SNR_WINDOW) {
+      return in ? v + rs * t : v;
+    } else if constexpr (MODE == ABD_INJECT_HALF_MIX) {
+      return in ? (v + t) / 2.0f : v / 2.0f;
+    } else {
+      const float sv = rs * v;
+      return in ? (sv + t) / (rs + 1.0f) : sv / (rs + 1.0f);
+    }
+  } else {
+    return v;
+  }
+}
+
+// Frames 2(p0+f), 2(p0+f)+1 of one utterance -> z = (a + i b) * (chirp | window), f < np,
+// zero-padded to M.  Groups of G elements per thread: all sample / chirp loads of a group
+// are issued before the first LDS store.  INTERIOR: every frame of the item lies inside the
+// signal (no padding, both frames of every pair exist), so sample addresses are affine.
+template <int M, int NN, int PP, bool BLUE, int MODE, bool INTERIOR>
+__device__ __forceinline__ void load_frames(float2* __restrict__ buf, const float* __restrict__ x, const MfccDev& p,
+                                            const InjDev& inj, int pos, float rs, int p0, int np) {
+  constexpr int TOT = PP * M;
+  constexpr int ITERS = (TOT + kThreads - 1) / kThreads;
+  constexpr int G = 8;
+  const int L = (int)p.L;
+  const bool refl = p.pad_mode != ABD_PAD_CONSTANT;
+  const int hop = p.hop;
+#pragma unroll
+  for (int g0 = 0; g0 < ITERS; g0 += G) {
+    float a[G], b[G];
+    float2 c[G];
+    bool ok[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int idx = ltid() + (g0 + q) * kThreads;
+      const int f = (PP == 1) ? 0 : idx / M;
+      const int n = idx - f * M;
+      ok[q] = (g0 + q < ITERS) && (idx < TOT) && (n < NN) && (PP == 1 || INTERIOR || f < np);
+      const int t0 = 2 * (p0 + f);
+      const int i0 = t0 * hop + n - p.pad, i1 = i0 + hop;
+      if (p.ablate & 1) {
+        a[q] = (float)n;
+        b[q] = (float)t0;
+      } else if constexpr (INTERIOR) {
+        // PP == 1: iterations wholly below NN load at base + immediate, wholly above NN load
+        // nothing; only the straddling one clamps (its n >= NN lanes are discarded).
+        const int it = g0 + q;
+        const bool full = PP == 1 && (it + 1) * kThreads <= NN;
+        const bool dead = PP == 1 && it * kThreads >= NN;
+        if (dead) {
+          a[q] = 0.0f;
+          b[q] = 0.0f;
+        } else {
+          const int s0 = full ? i0 : min(i0, L - 1 - hop);
+          a[q] = fsample<MODE>(x, inj, s0, pos, rs);
+          b[q] = fsample<MODE>(x, inj, s0 + hop, pos, rs);
+        }
+      } else {
+        const bool okb = t0 + 1 < p.T;
+        int s0 = refl ? abs(i0) : i0, s1 = refl ? abs(i1) : i1;
+        if (refl) {
+          s0 = (s0 >= L) ? 2 * (L - 1) - s0 : s0;
+          s1 = (s1 >= L) ? 2 * (L - 1) - s1 : s1;
+        }
+        const bool in0 = refl || (i0 >= 0 && i0 < L), in1 = refl || (i1 >= 0 && i1 < L);
+        s0 = min(max(s0, 0), L - 1);
+        s1 = min(max(s1, 0), L - 1);
+        a[q] = in0 ? fsample<MODE>(x, inj, s0, pos, rs) : 0.0f;
+        b[q] = (in1 && okb) ? fsample<MODE>(x, inj, s1, pos, rs) : 0.0f;
+      }
+      const int nn = min(n, NN - 1);
+      if constexpr (BLUE) {
+        c[q] = p.chirp_in[nn];
+      } else {
+        const float w = p.window[nn];
+        c[q] = make_float2(w, w);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int idx = ltid() + (g0 + q) * kThreads;
+      if ((g0 + q < ITERS) && idx < TOT) {
+        float2 z;
+        if constexpr (BLUE) z = cmul(make_float2(a[q], b[q]), c[q]);
+        else z = make_float2(a[q] * c[q].x, b[q] * c[q].y);
+        buf[pidx(idx)] = ok[q] ? z : make_float2(0.0f, 0.0f);
+      }
+    }
+  }
+}
+
+template <int M, int NN, int PP, bool BLUE, int MODE>
+__device__ __forceinline__ void load_item(float2* buf, const float* x, const MfccDev& p, const InjDev& inj, int pos,
+                                          float rs, int p0, int np) {
+  const int first = 2 * p0 * p.hop - p.pad;
+  const int last_t = 2 * (p0 + PP) - 1;
+  const bool interior = np == PP && first >= 0 && last_t < p.T && last_t * p.hop - p.pad + NN <= (int)p.L;
+  if (interior) load_frames<M, NN, PP, BLUE, MODE, true>(buf, x, p, inj, pos, rs, p0, np);
+  else load_frames<M, NN, PP, BLUE, MODE, false>(buf, x, p, inj, pos, rs, p0, np);
+}
+
+// Persistent blocks walk a contiguous range of (utterance, chunk) work items; each item is
+// PP pairs of frames of one utterance.  Per item:
+//   gather + inject + chirp/window -> FFT (-> pointwise * vhat -> FFT, Bluestein)
+//   -> in-place power |A_k|^2, |B_k|^2 (Bluestein output chirp fused)
+//   -> mel by half-filter slots (2 per filter, balanced), halves combined by a lane swap
+//   -> 10 log10 -> ws_db, per-item max -> ws_max.
+template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
 __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
                                                                  int64_t row_stride,
                                                                  const int32_t* __restrict__ rows, int64_t batch,
                                                                  InjDev inj, const float* __restrict__ rowscale,
                                                                  float* __restrict__ ws_db,
-                                                                 float* __restrict__ ws_max) {
+                                                                 float* __restrict__ ws_max,
+                                                                 unsigned* __restrict__ queue) {
+  constexpr int NT = 2 * R0 * R1;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* tw = lds;
-  float2* buf = lds + M;
+  float2* buf = lds + NT;
+  float* wl = reinterpret_cast<float*>(lds + NT + PP * (M + M / 16));
   __shared__ float red[kThreads / kWave];
-  for (int i = threadIdx.x; i < M; i += kThreads) tw[i] = p.tw[i];
+  for (int i = ltid(); i < NT; i += kThreads) tw[i] = p.ftw[i];
+  for (int i = ltid(); i < p.mel2_total; i += kThreads) wl[i] = p.mel2_w[i];
+  __shared__ unsigned s_item;
   const int chunks = p.chunks;
-  const int64_t n_items = batch * chunks;
-  const int64_t per = (n_items + gridDim.x - 1) / gridDim.x;
-  const int64_t i0 = blockIdx.x * per, i1 = min(n_items, i0 + per);
+  const unsigned n_items = (unsigned)(batch * chunks);
   const int P = (p.T + 1) / 2;
-  for (int64_t item = i0; item < i1; ++item) {
+  constexpr int nf = NN / 2 + 1;
+  const int S = 2 * p.n_mels;
+  // Dynamic item queues (zeroed by the host before the launch): no static split, so blocks
+  // that become resident late cannot leave a tail.  kQueues counters on separate 256-B
+  // lines, each owning a contiguous 1/kQueues of the items; a block pulls from its home
+  // queue, then steals from the others.  Thread 0 grabs the next item while the block
+  // works on the current one.
+  const unsigned qlen = (n_items + kQueues - 1) / kQueues;
+  unsigned home = blockIdx.x % kQueues;
+  auto grab = [&]() -> unsigned {
+    for (int t = 0; t < kQueues; ++t) {
+      const unsigned q = (home + t) % kQueues;
+      const unsigned v = atomicAdd(queue + q * kQueueStride, 1u);
+      const unsigned it = q * qlen + v;
+      if (v < qlen && it < n_items) {
+        home = q;
+        return it;
+      }
+    }
+    return ~0u;
+  };
+  if (threadIdx.x == 0) s_item = grab();
+  __syncthreads();  // also publishes the staged tables
+  unsigned item = s_item;
+  while (item != ~0u) {
+    unsigned next = 0;
+    if (threadIdx.x == 0) next = grab();
     const int64_t u = item / chunks;
     const int c = (int)(item - u * chunks);
     const int64_t row = rows ? rows[u] : u;
@@ -590,81 +786,96 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
     const float rs = (rowscale != nullptr) ? rowscale[u] : 0.0f;
     const int p0 = c * PP;
     const int np = min(PP, P - p0);
-    __syncthreads();  // previous item fully consumed (and twiddles staged on the first pass)
-    for (int idx = threadIdx.x; idx < PP * M; idx += kThreads) {
-      const int f = idx / M;
-      const int n = idx - f * M;
-      float2 z = make_float2(0.0f, 0.0f);
-      if (f < np && n < p.N) {
-        const int t0 = 2 * (p0 + f), t1 = t0 + 1;
-        const bool skip = p.ablate & 1;
-        const float a = skip ? (float)n : padded_sample(x, (int64_t)t0 * p.hop + n, p, inj, pois, pos, rs);
-        const float b = skip ? (float)t1 : ((t1 < p.T) ? padded_sample(x, (int64_t)t1 * p.hop + n, p, inj, pois, pos, rs) : 0.0f);
-        if constexpr (BLUE) {
-          z = cmul(make_float2(a, b), p.chirp_in[n]);
-        } else {
-          const float w = p.window[n];
-          z = make_float2(a * w, b * w);
-        }
-      }
-      buf[idx] = z;
+    switch (pois ? inj.mode : ABD_INJECT_NONE) {
+      case ABD_INJECT_ADD: load_item<M, NN, PP, BLUE, ABD_INJECT_ADD>(buf, x, p, inj, pos, rs, p0, np); break;
+      case ABD_INJECT_SNR_WINDOW:
+        load_item<M, NN, PP, BLUE, ABD_INJECT_SNR_WINDOW>(buf, x, p, inj, pos, rs, p0, np);
+        break;
+      case ABD_INJECT_HALF_MIX:
+        load_item<M, NN, PP, BLUE, ABD_INJECT_HALF_MIX>(buf, x, p, inj, pos, rs, p0, np);
+        break;
+      case ABD_INJECT_DEPLOY: load_item<M, NN, PP, BLUE, ABD_INJECT_DEPLOY>(buf, x, p, inj, pos, rs, p0, np); break;
+      default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE>(buf, x, p, inj, pos, rs, p0, np); break;
     }
     __syncthreads();
-    if (!(p.ablate & 2)) fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
-    if constexpr (BLUE) {
-      if (!(p.ablate & 2)) fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
-      // X[k] = conj(w[k] R[k]) / M for k < N
-      for (int idx = threadIdx.x; idx < np * p.N; idx += kThreads) {
-        const int f = idx / p.N;
-        const int k = idx - f * p.N;
-        const float2 r = cmul(p.chirp_out[k], buf[f * M + k]);
-        buf[f * M + k] = make_float2(r.x, -r.y);
-      }
-      __syncthreads();
+    if (!(p.ablate & 2)) {
+      fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+      if constexpr (BLUE) fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
     }
-    // two real spectra from the packed one -> power -> mel -> dB
     float lmax = -INFINITY;
-    for (int idx = threadIdx.x; idx < ((p.ablate & 4) ? 0 : np * p.n_mels); idx += kThreads) {
-      const int f = idx / p.n_mels;
-      const int m = idx - f * p.n_mels;
-      const float2* Z = buf + f * M;
-      const int st = p.mel_start[m], cnt = p.mel_count[m];
-      const float* w = p.mel_w + p.mel_off[m];
-      float acc_a = 0.0f, acc_b = 0.0f;
-      for (int i = 0; i < cnt; ++i) {
-        const int k = st + i;
-        const int kn = (k == 0) ? 0 : p.N - k;
-        const float2 P1 = Z[k], Q = Z[kn];
+    if (!(p.ablate & 4)) {
+      // Power of the two real spectra, written over Z[k] (k <= N/2).  Z[k] is read only by
+      // the thread that owns bin k (Z[N-k] with N-k > N/2 is never written), so no barrier
+      // is needed between the reads and the in-place writes.
+      for (int idx = ltid(); idx < np * nf; idx += kThreads) {
+        const int f = idx / nf;
+        const int k = idx - f * nf;
+        const int kn = (k == 0) ? 0 : NN - k;
+        float2* Z = buf + f * (M + M / 16);
+        float2 P1 = Z[pidx(k)], Q = Z[pidx(kn)];
+        if constexpr (BLUE) {  // X[k] = conj(w[k] R[k]) / M
+          const float2 a = cmul(p.chirp_out[k], P1), b = cmul(p.chirp_out[kn], Q);
+          P1 = make_float2(a.x, -a.y);
+          Q = make_float2(b.x, -b.y);
+        }
         const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
         const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
-        acc_a = fmaf(ar * ar + ai * ai, w[i], acc_a);
-        acc_b = fmaf(br * br + bi * bi, w[i], acc_b);
+        Z[pidx(k)] = make_float2(ar * ar + ai * ai, br * br + bi * bi);
       }
-      const int ta = 2 * (p0 + f);
-      const float da = 10.0f * log10f(fmaxf(acc_a, 1e-10f));
-      ws_db[((int64_t)u * p.T + ta) * p.n_mels + m] = da;
-      lmax = fmaxf(lmax, da);
-      if (ta + 1 < p.T) {
-        const float db = 10.0f * log10f(fmaxf(acc_b, 1e-10f));
-        ws_db[((int64_t)u * p.T + ta + 1) * p.n_mels + m] = db;
-        lmax = fmaxf(lmax, db);
+      __syncthreads();
+      const int tot = np * S;
+      const int rounds = (tot + kThreads - 1) / kThreads;
+      const int hp = p.mel2_hp;
+      const int wlast = p.mel2_total - 1;
+      for (int rd = 0; rd < rounds; ++rd) {  // uniform: every lane reaches the shuffles
+        const int g = ltid() + rd * kThreads;
+        const bool act = g < tot;
+        const int gg = act ? g : 0;
+        const int f = gg / S;
+        const int sl = gg - f * S;
+        const int4 meta = p.mel2_meta[sl];  // (start, count, weight offset, -)
+        const float2* Z = buf + f * (M + M / 16);
+        float sa = 0.0f, sb = 0.0f;
+        for (int i0 = 0; i0 < hp; i0 += 8) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int i = i0 + q;
+            const int k = min(meta.x + i, nf - 1);
+            const float w = (i < meta.y) ? wl[min(meta.z + i, wlast)] : 0.0f;
+            const float2 pw = Z[pidx(k)];
+            sa = fmaf(pw.x, w, sa);
+            sb = fmaf(pw.y, w, sb);
+          }
+        }
+        sa += __shfl_xor(sa, 1);
+        sb += __shfl_xor(sb, 1);
+        const int h = sl & 1;
+        const int t = 2 * (p0 + f) + h;
+        if (act && t < p.T) {
+          const float d = 10.0f * log10f(fmaxf(h ? sb : sa, 1e-10f));
+          ws_db[((int64_t)u * p.T + t) * p.n_mels + (sl >> 1)] = d;
+          lmax = fmaxf(lmax, d);
+        }
       }
     }
     lmax = abd::wave_max(lmax);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = lmax;
+    if ((ltid() & 63) == 0) red[ltid() / kWave] = lmax;
     __syncthreads();
     if (threadIdx.x == 0) {
       float mm = red[0];
       for (int i = 1; i < kThreads / kWave; ++i) mm = fmaxf(mm, red[i]);
       ws_max[u * chunks + c] = mm;
+      s_item = next;
     }
+    __syncthreads();  // s_item published; this item's LDS reads are complete
+    item = s_item;
   }
 }
 
 struct FastPlan {
-  int M, N, bluestein, pp;
+  int M, N, bluestein, pp, r0, r1;
 };
-constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1}, {2048, 2048, 0, 4}, {400, 400, 0, 13}};
+constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1, 16, 16}, {2048, 2048, 0, 4, 16, 16}, {400, 400, 0, 13, 16, 25}};
 
 const FastPlan* find_fast(int M, int N, int blue) {
   for (const auto& f : kFastPlans)
@@ -672,33 +883,46 @@ const FastPlan* find_fast(int M, int N, int blue) {
   return nullptr;
 }
 
-template <int M, int R0, int R1, int R2, int PP, bool BLUE>
+template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
 int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
-                const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, hipStream_t s) {
-  const size_t lds = (size_t)(PP + 1) * M * sizeof(float2);
-  static bool attr_set = false;
-  if (!attr_set) {
-    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&stft_mel_fast_kernel<M, R0, R1, R2, PP, BLUE>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr_set = true;
+                const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
+                hipStream_t s) {
+  auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE>;
+  static_assert(M % 16 == 0, "padded LDS layout needs M % 16 == 0");
+  const size_t lds = (size_t)(2 * R0 * R1 + PP * (M + M / 16)) * sizeof(float2) + (size_t)((d.mel2_total + 3) & ~3) * 4;
+  // residency from the occupancy API (VGPRs + LDS), cached per LDS size
+  static size_t cached_lds = 0;
+  static int cached_blocks = 0, n_cu = 0;
+  if (cached_lds != lds) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    int dev = 0, nb = 0;
+    ABD_HIP(hipGetDevice(&dev));
+    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kern), kThreads, lds));
+    cached_blocks = std::max(1, nb);
+    cached_lds = lds;
   }
-  const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 64)));
   const int64_t items = batch * d.chunks;
-  const int grid = (int)std::min<int64_t>(items, 256LL * per_cu);
-  stft_mel_fast_kernel<M, R0, R1, R2, PP, BLUE><<<grid, kThreads, lds, s>>>(d, wave, row_stride, rows, batch, ij,
-                                                                            rowscale, ws_db, ws_max);
+  const int grid = (int)std::min<int64_t>(items, (int64_t)n_cu * cached_blocks);
+  ABD_HIP(hipMemsetAsync(queue, 0, kQueues * kQueueStride * sizeof(unsigned), s));
+  kern<<<grid, kThreads, lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue);
   ABD_LAUNCH_CHECK();
   return 0;
 }
 
 int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
-                  const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, hipStream_t s) {
-  if (d.M == 2304 && d.bluestein)
-    return launch_fast<2304, 16, 16, 9, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
-  if (d.M == 2048 && !d.bluestein)
-    return launch_fast<2048, 16, 16, 8, 4, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
-  if (d.M == 400 && !d.bluestein)
-    return launch_fast<400, 16, 25, 1, 13, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s);
+                  const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
+                  hipStream_t s) {
+  if (d.M == 2304 && d.N == 1103 && d.bluestein)
+    return launch_fast<2304, 1103, 16, 16, 9, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
+                                                       queue, s);
+  if (d.M == 2048 && d.N == 2048 && !d.bluestein)
+    return launch_fast<2048, 2048, 16, 16, 8, 4, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db,
+                                                        ws_max, queue, s);
+  if (d.M == 400 && d.N == 400 && !d.bluestein)
+    return launch_fast<400, 400, 16, 25, 1, 13, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
+                                                       queue, s);
   return -1;
 }
 
@@ -922,6 +1146,30 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     for (int k = lo; k <= hi; ++k) mw.push_back((float)fb[(size_t)k * n_mels + m]);
   }
   if (mw.empty()) mw.push_back(0.0f);
+  // half-filter slots for the fast kernel: filter m's support split into two contiguous halves
+  std::vector<int4> meta2(2 * (size_t)n_mels);
+  std::vector<float> mw2;
+  int hmax = 0;
+  for (int m = 0; m < n_mels; ++m) {
+    const int lo = mstart[m], cnt = mcount[m], c0 = (cnt + 1) / 2;
+    for (int h = 0; h < 2; ++h) {
+      const int st = lo + (h ? c0 : 0), c = h ? cnt - c0 : c0;
+      meta2[2 * m + h] = make_int4(st, c, (int)mw2.size(), 0);
+      for (int k = st; k < st + c; ++k) mw2.push_back((float)fb[(size_t)k * n_mels + m]);
+      hmax = std::max(hmax, c);
+    }
+  }
+  if (mw2.empty()) mw2.push_back(0.0f);
+  d.mel2_total = (int)mw2.size();
+  d.mel2_hp = std::max(8, (hmax + 7) / 8 * 8);
+  // fast-kernel twiddles: W_{R0 R1}^e and W_M^k, e, k < R0 R1
+  const int r01 = fp ? fp->r0 * fp->r1 : 1;
+  std::vector<float2> ftw(2 * (size_t)r01);
+  for (int e = 0; e < r01; ++e) {
+    const double a = -2.0 * M_PI * e / r01, b = -2.0 * M_PI * e / M;
+    ftw[e] = make_float2((float)cos(a), (float)sin(a));
+    ftw[r01 + e] = make_float2((float)cos(b), (float)sin(b));
+  }
   std::vector<float> dct((size_t)n_mels * n_mfcc);
   for (int m = 0; m < n_mels; ++m)
     for (int c = 0; c < n_mfcc; ++c) {
@@ -951,6 +1199,12 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   sz += al(mw.size() * sizeof(float));
   size_t off_dct = sz;
   sz += al(dct.size() * sizeof(float));
+  size_t off_ftw = sz;
+  sz += al(ftw.size() * sizeof(float2));
+  size_t off_m2 = sz;
+  sz += al(meta2.size() * sizeof(int4));
+  size_t off_w2 = sz;
+  sz += al(mw2.size() * sizeof(float));
   std::vector<char> host(sz, 0);
   memcpy(&host[off_tw], tw.data(), M * sizeof(float2));
   memcpy(&host[off_ci], chirp_in.data(), N * sizeof(float2));
@@ -962,6 +1216,9 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   memcpy(&host[off_mo], moff.data(), n_mels * sizeof(int));
   memcpy(&host[off_mw], mw.data(), mw.size() * sizeof(float));
   memcpy(&host[off_dct], dct.data(), dct.size() * sizeof(float));
+  memcpy(&host[off_ftw], ftw.data(), ftw.size() * sizeof(float2));
+  memcpy(&host[off_m2], meta2.data(), meta2.size() * sizeof(int4));
+  memcpy(&host[off_w2], mw2.data(), mw2.size() * sizeof(float));
   hipError_t e = hipMalloc(&pl->block, sz);
   if (e != hipSuccess) {
     delete pl;
@@ -986,6 +1243,9 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.mel_off = reinterpret_cast<const int*>(b + off_mo);
   d.mel_w = reinterpret_cast<const float*>(b + off_mw);
   d.dct = reinterpret_cast<const float*>(b + off_dct);
+  d.ftw = reinterpret_cast<const float2*>(b + off_ftw);
+  d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
+  d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
   *plan = pl;
   return ABD_OK;
 }
@@ -1013,7 +1273,7 @@ size_t abd_mfcc_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch) {
   const MfccDev& d = plan->dev;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   return al((size_t)batch * d.T * d.n_mels * sizeof(float)) + al((size_t)batch * d.chunks * sizeof(float)) +
-         al((size_t)batch * sizeof(float));
+         al((size_t)batch * sizeof(float)) + kQueues * kQueueStride * sizeof(unsigned);  // + item queues
 }
 
 static InjDev make_inj(const abd_inject* inj) {
@@ -1066,6 +1326,9 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   float* ws_max = reinterpret_cast<float*>(ws + al((size_t)batch * d.T * d.n_mels * sizeof(float)));
   float* ws_scale = reinterpret_cast<float*>(ws + al((size_t)batch * d.T * d.n_mels * sizeof(float)) +
                                              al((size_t)batch * d.chunks * sizeof(float)));
+  unsigned* queue = reinterpret_cast<unsigned*>(ws + al((size_t)batch * d.T * d.n_mels * sizeof(float)) +
+                                                al((size_t)batch * d.chunks * sizeof(float)) +
+                                                al((size_t)batch * sizeof(float)));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float* rowscale = nullptr;
   if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY) {
@@ -1078,7 +1341,7 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   const size_t lds = 2 * (size_t)d.ppb * d.M * sizeof(float2);
   abd::prof_begin(abd::PH_STFT_MEL, s);
   if (d.fast) {
-    if (dispatch_fast(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, s) != 0) return -1;
+    if (dispatch_fast(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue, s) != 0) return -1;
   } else {
     stft_mel_kernel<<<dim3((unsigned)nblk), dim3(kThreads), lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale,
                                                                     ws_db, ws_max);
