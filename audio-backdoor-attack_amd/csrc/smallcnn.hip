@@ -390,93 +390,193 @@ struct PoolArgs {
   int nblk;
 };
 
-__device__ __forceinline__ int pool_argmax(const PoolArgs& a, int b, int ho, int wo, int c, float4 cf, float& best) {
-  best = -INFINITY;
-  int arg = -1;
-  for (int i = 0; i < a.kh; ++i) {
-    const int h = ho * a.sh - a.ph + i;
-    if (h < 0 || h >= a.H) continue;
-    for (int j = 0; j < a.kw; ++j) {
-      const int w = wo * a.sw - a.pw + j;
-      if (w < 0 || w >= a.W) continue;
-      const float y = fmaf(cf.z, a.r[(((int64_t)b * a.H + h) * a.W + w) * a.C + c], cf.w);
-      if (y > best) {
-        best = y;
-        arg = h * a.W + w;
+// Pool windows tile the grid (kernel == stride for both pools), so the pool kernels run one
+// thread per (window, 4 channels): the argmax is found once per window with int32 index
+// math and float4 channel vectors, and the backward kernel writes every element of its
+// window.  Windows are enumerated over the extended grid Hx x Wx that also covers rows /
+// columns no real window reaches (pool3 drops the last conv3 row): those get dy = 0.
+struct WinIdx {
+  int b, ho, wo, cg;
+};
+
+__device__ __forceinline__ WinIdx win_index(int o, int CG, int Wx, int Hx) {
+  WinIdx r;
+  r.cg = o % CG;
+  int q = o / CG;
+  r.wo = q % Wx;
+  q /= Wx;
+  r.ho = q % Hx;
+  r.b = q / Hx;
+  return r;
+}
+
+__device__ __forceinline__ float f4get(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int i, float x) {
+  if (i == 0) v.x = x;
+  else if (i == 1) v.y = x;
+  else if (i == 2) v.z = x;
+  else v.w = x;
+}
+
+// argmax (first maximum in scan order, strict '>') of bn(r) over the window, per channel;
+// arg = window slot i*kw + j, -1 if empty.  Loads each window element once.
+__device__ __forceinline__ void win_argmax(const PoolArgs& a, int b, int ho, int wo, int c0, const float4* cf,
+                                           float4 (&rv)[4], bool (&in)[4], float (&best)[4], int (&arg)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    best[q] = -INFINITY;
+    arg[q] = -1;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int slot = i * 2 + j;
+      const int h = ho * a.sh - a.ph + i, w = wo * a.sw - a.pw + j;
+      in[slot] = (i < a.kh) && (j < a.kw) && h >= 0 && h < a.H && w >= 0 && w < a.W;
+      rv[slot] = in[slot] ? *reinterpret_cast<const float4*>(a.r + ((b * a.H + h) * a.W + w) * a.C + c0)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+  for (int slot = 0; slot < 4; ++slot) {
+    if (!in[slot]) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float y = fmaf(cf[q].z, f4get(rv[slot], q), cf[q].w);
+      if (y > best[q]) {
+        best[q] = y;
+        arg[q] = slot;
       }
     }
   }
-  return arg;
 }
 
-__device__ __forceinline__ int64_t pooled_index(const PoolArgs& a, int b, int ho, int wo, int c) {
-  if (a.flat_n > 0) return (int64_t)b * a.flat_n + ((int64_t)c * a.Ho + ho) * a.Wo + wo;
-  return (((int64_t)b * a.Ho + ho) * a.Wo + wo) * a.C + c;
+__device__ __forceinline__ int pooled_index(const PoolArgs& a, int b, int ho, int wo, int c) {
+  if (a.flat_n > 0) return b * a.flat_n + (c * a.Ho + ho) * a.Wo + wo;
+  return ((b * a.Ho + ho) * a.Wo + wo) * a.C + c;
+}
+
+// per-channel partial sums of NV values over the threads sharing a channel group
+// (thread t holds channels 4*(t % CG) .. +3); part[(j*C + c)*nblk + blk]
+template <int NV>
+__device__ __forceinline__ void cgroup_partials(float (&v)[NV][4], int C, float* part, int nblk, int blk) {
+  __shared__ float red[NV * 4][kT];
+  const int t = threadIdx.x, CG = C / 4;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[j * 4 + q][t] = v[j][q];
+  __syncthreads();
+  for (int o = t; o < NV * C; o += kT) {
+    const int j = o / C, c = o - j * C;
+    const int cg = c / 4, q = c % 4;
+    float sacc = 0.0f;
+    for (int u = cg; u < kT; u += CG) sacc += red[j * 4 + q][u];
+    part[((int64_t)j * C + c) * nblk + blk] = sacc;
+  }
 }
 
 __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
-  const int64_t total = (int64_t)a.B * a.Ho * a.Wo * a.C;
-  for (int64_t o = blockIdx.x * (int64_t)kT + threadIdx.x; o < total; o += (int64_t)gridDim.x * kT) {
-    const int c = (int)(o % a.C);
-    int64_t q = o / a.C;
-    const int wo = (int)(q % a.Wo);
-    q /= a.Wo;
-    const int ho = (int)(q % a.Ho);
-    const int b = (int)(q / a.Ho);
-    float best;
-    pool_argmax(a, b, ho, wo, c, a.coef[c], best);
-    const int64_t oi = pooled_index(a, b, ho, wo, c);
-    a.out[oi] = drop_apply(a.drop, oi, best);
-  }
-}
-
-__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) {
-  const int64_t total = (int64_t)a.B * a.Ho * a.Wo * a.C;
-  const int c = threadIdx.x % a.C;  // fixed per thread: grid stride is a multiple of C
-  const float4 cf = a.coef[c];
-  float v[2] = {0.0f, 0.0f};
-  for (int64_t o = blockIdx.x * (int64_t)kT + threadIdx.x; o < total; o += (int64_t)gridDim.x * kT) {
-    int64_t q = o / a.C;
-    const int wo = (int)(q % a.Wo);
-    q /= a.Wo;
-    const int ho = (int)(q % a.Ho);
-    const int b = (int)(q / a.Ho);
-    float best;
-    const int arg = pool_argmax(a, b, ho, wo, c, cf, best);
-    const float dy = a.dp[pooled_index(a, b, ho, wo, c)];
-    const float rv = a.r[(((int64_t)b * a.H) * a.W + arg) * a.C + c];
-    v[0] += dy;
-    v[1] = fmaf(dy, (rv - cf.x) * cf.y, v[1]);
-  }
-  channel_partials<2>(v, a.C, a.part, a.nblk, blockIdx.x);
-}
-
-// dz = relu'(r) * BN backward(dy scattered to the argmax); bias-grad partials
-__global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a) {
-  const int64_t total = (int64_t)a.B * a.H * a.W * a.C;
-  const int c = threadIdx.x % a.C;
-  const float4 cf = a.coef[c];
-  const BCoef bc = a.bcoef[c];
-  float v[1] = {0.0f};
-  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    int64_t q = e / a.C;
-    const int w = (int)(q % a.W);
-    q /= a.W;
-    const int h = (int)(q % a.H);
-    const int b = (int)(q / a.H);
-    const int ho = (h + a.ph) / a.sh, wo = (w + a.pw) / a.sw;
-    float dy = 0.0f;
-    if (ho < a.Ho && wo < a.Wo) {
-      float best;
-      const int arg = pool_argmax(a, b, ho, wo, c, cf, best);
-      if (arg == h * a.W + w) dy = a.dp[pooled_index(a, b, ho, wo, c)];
+  const int CG = a.C / 4;
+  const int total = a.B * a.Ho * a.Wo * CG;
+  for (int o = blockIdx.x * kT + threadIdx.x; o < total; o += gridDim.x * kT) {
+    const WinIdx wi = win_index(o, CG, a.Wo, a.Ho);
+    const int c0 = wi.cg * 4;
+    float4 cf[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cf[q] = a.coef[c0 + q];
+    float4 rv[4];
+    bool in[4];
+    float best[4];
+    int arg[4];
+    win_argmax(a, wi.b, wi.ho, wi.wo, c0, cf, rv, in, best, arg);
+    if (a.flat_n > 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oi = pooled_index(a, wi.b, wi.ho, wi.wo, c0 + q);
+        a.out[oi] = drop_apply(a.drop, oi, best[q]);
+      }
+    } else {
+      const int oi = pooled_index(a, wi.b, wi.ho, wi.wo, c0);
+      float4 r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f4set(r, q, drop_apply(a.drop, oi + q, best[q]));
+      *reinterpret_cast<float4*>(a.out + oi) = r;
     }
-    const float rv = a.r[e];
-    const float dz = rv > 0.0f ? bn_dx(dy, rv, cf, bc) : 0.0f;
-    a.dz[e] = dz;
-    v[0] += dz;
   }
-  channel_partials<1>(v, a.C, a.part, a.nblk, blockIdx.x);
+}
+
+// BN backward sums over pooled outputs: sum dy, sum dy * xhat(r at the argmax)
+__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) {
+  const int CG = a.C / 4;
+  const int total = a.B * a.Ho * a.Wo * CG;
+  const int c0 = (threadIdx.x % CG) * 4;  // fixed per thread: grid stride is a multiple of CG
+  float4 cf[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cf[q] = a.coef[c0 + q];
+  float v[2][4] = {};
+  for (int o = blockIdx.x * kT + threadIdx.x; o < total; o += gridDim.x * kT) {
+    const WinIdx wi = win_index(o, CG, a.Wo, a.Ho);
+    float4 rv[4];
+    bool in[4];
+    float best[4];
+    int arg[4];
+    win_argmax(a, wi.b, wi.ho, wi.wo, c0, cf, rv, in, best, arg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dy = a.dp[pooled_index(a, wi.b, wi.ho, wi.wo, c0 + q)];
+      float r = 0.0f;
+#pragma unroll
+      for (int slot = 0; slot < 4; ++slot) r = (arg[q] == slot) ? f4get(rv[slot], q) : r;
+      v[0][q] += dy;
+      v[1][q] = fmaf(dy, (r - cf[q].x) * cf[q].y, v[1][q]);
+    }
+  }
+  cgroup_partials<2>(v, a.C, a.part, a.nblk, blockIdx.x);
+}
+
+// dz = relu'(r) * BN backward(dy scattered to the argmax) over every element of each
+// (extended) window; bias-grad partials
+__global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a, int Hx, int Wx) {
+  const int CG = a.C / 4;
+  const int total = a.B * Hx * Wx * CG;
+  const int c0 = (threadIdx.x % CG) * 4;
+  float4 cf[4];
+  BCoef bc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    cf[q] = a.coef[c0 + q];
+    bc[q] = a.bcoef[c0 + q];
+  }
+  float v[1][4] = {};
+  for (int o = blockIdx.x * kT + threadIdx.x; o < total; o += gridDim.x * kT) {
+    const WinIdx wi = win_index(o, CG, Wx, Hx);
+    const bool real = wi.ho < a.Ho && wi.wo < a.Wo;
+    float4 rv[4];
+    bool in[4];
+    float best[4];
+    int arg[4];
+    win_argmax(a, wi.b, wi.ho, wi.wo, c0, cf, rv, in, best, arg);
+    float dy[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dy[q] = real ? a.dp[pooled_index(a, wi.b, wi.ho, wi.wo, c0 + q)] : 0.0f;
+#pragma unroll
+    for (int slot = 0; slot < 4; ++slot) {
+      if (!in[slot]) continue;
+      const int h = wi.ho * a.sh - a.ph + slot / 2, w = wi.wo * a.sw - a.pw + slot % 2;
+      float4 dz;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float r = f4get(rv[slot], q);
+        const float d = (real && arg[q] == slot) ? dy[q] : 0.0f;
+        const float z = r > 0.0f ? bn_dx(d, r, cf[q], bc[q]) : 0.0f;
+        f4set(dz, q, z);
+        v[0][q] += z;
+      }
+      *reinterpret_cast<float4*>(a.dz + ((wi.b * a.H + h) * a.W + w) * a.C + c0) = dz;
+    }
+  }
+  cgroup_partials<1>(v, a.C, a.part, a.nblk, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ fp32 MFMA GEMMs
@@ -722,6 +822,97 @@ __global__ void __launch_bounds__(kT) gemm_tn_kernel(TNArgs a) {
     for (int r = 0; r < 16; ++r) {
       const int n = n0 + ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (n < a.N && k < a.Ktot) slab[(int64_t)n * a.Ktot + k] = acc[i][r];
+    }
+  }
+}
+
+// 2x2 convolution weight gradient by output-row chunks.
+//   dW[n][t*CIN + ci] = sum_m dz[m][n] * src[row(m) + tap t][ci]
+// A chunk is R consecutive output rows of one utterance: its dz rows (R*Wo*NB floats) and
+// the R+1 source rows the four taps read ((R+1)*Ws*CIN floats) are both contiguous in
+// NHWC, so they are copied into LDS with global_load_lds (no VGPR staging, no index
+// math) into one of two buffers while the block runs the MFMAs of the previous chunk.
+// The taps are then constant LDS offsets.  Each wave owns TPW 32x32 accumulator tiles of
+// one n-tile; each block sums a contiguous range of chunks into its slab, reduced later
+// in slab order (deterministic).
+struct WGArgs {
+  const float* dz;   // (B, Ho, Wo, NB)
+  const float* src;  // (B, Hs, Ws, CIN), Hs >= Ho + 1, Ws >= Wo + 1
+  int Ho, Wo, Hs, Ws;
+  int R, cpb, nchunks, per;
+  int dsz, bsz;      // LDS floats: dz part (16-B aligned) and one whole buffer
+  float* slab;       // [gridDim.x][NB][4*CIN]
+};
+
+__device__ __forceinline__ void glds_copy(const float* g, float* l, int n16) {
+  // n16 16-byte pieces, lane-linear: wave-instruction j of wave w copies pieces
+  // (j*kT + w*64) .. +63 into the same offsets of l
+  const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
+  for (int i0 = 0; i0 < n16; i0 += kT) {
+    const int i = i0 + wbase + lane;
+    if (i < n16)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 4 * i),
+                                       (__attribute__((address_space(3))) void*)(l + 4 * (i0 + wbase)), 16, 0, 0);
+  }
+}
+
+template <int NB, int CIN>
+__global__ void __launch_bounds__(kT) conv_wgrad_rows_kernel(WGArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_wg[];
+  constexpr int KT = 4 * CIN / 32, TILES = (NB / 32) * KT, TPW = TILES / 4;
+  static_assert(TILES % 4 == 0 && KT % TPW == 0, "a wave's tiles must share one n-tile");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, col = lane & 31;
+  const int nt = (wave * TPW) / KT;
+  int boff[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int kt = (wave * TPW + i) % KT;
+    const int tap = kt / (CIN / 32), cb = kt % (CIN / 32);
+    boff[i] = ((tap >> 1) * a.Ws + (tap & 1)) * CIN + cb * 32 + col;
+  }
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
+  auto stage = [&](int c, float* buf) {
+    const int b = c / a.cpb, h0 = (c - b * a.cpb) * a.R;
+    const int rows = min(a.R, a.Ho - h0);
+    glds_copy(a.dz + ((int64_t)b * a.Ho + h0) * a.Wo * NB, buf, rows * a.Wo * NB / 4);
+    glds_copy(a.src + ((int64_t)b * a.Hs + h0) * a.Ws * CIN, buf + a.dsz, (rows + 1) * a.Ws * CIN / 4);
+  };
+  if (c0 < c1) stage(c0, lds_wg);
+  for (int c = c0; c < c1; ++c) {
+    float* cur = lds_wg + ((c - c0) & 1) * a.bsz;
+    __syncthreads();  // chunk c landed (vmcnt(0) + barrier); the other buffer is free
+    if (c + 1 < c1) stage(c + 1, lds_wg + ((c + 1 - c0) & 1) * a.bsz);
+    const int h0 = (c % a.cpb) * a.R;
+    const int mcount = min(a.R, a.Ho - h0) * a.Wo;
+    const float* D = cur + nt * 32 + col;
+    const float* S = cur + a.dsz;
+    for (int mp = 0; mp < mcount; mp += 2) {
+      const int m = mp + half;
+      const bool ok = m < mcount;
+      const int hl = m / a.Wo, w = m - hl * a.Wo;
+      const float av = ok ? D[m * NB] : 0.0f;
+      const float* sp = S + (hl * a.Ws + w) * CIN;
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const float bv = ok ? sp[boff[i]] : 0.0f;
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i], 0, 0, 0);
+      }
+    }
+  }
+  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int k = ((wave * TPW + i) % KT) * 32 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      slab[(int64_t)n * (4 * CIN) + k] = acc[i][r];
     }
   }
 }
@@ -1086,6 +1277,10 @@ PoolArgs pool_args(const Geo& g, int layer, int64_t B) {
   return a;
 }
 
+// extended window grid of bn_bwd_apply_kernel (windows tile the input: kernel == stride)
+int win_ext_h(const PoolArgs& a) { return std::max(a.Ho, (a.H + a.ph + a.sh - 1) / a.sh); }
+int win_ext_w(const PoolArgs& a) { return std::max(a.Wo, (a.W + a.pw + a.sw - 1) / a.sw); }
+
 NTArgs conv_fwd_args(const float* src, int Hs, int Ws, int Cs, int Ho, int Wo, int64_t B, const float* Bw, int N,
                      const float* bias, float* out) {
   NTArgs a{};
@@ -1143,6 +1338,54 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
   a.mchunk = (a.mchunk + 31) / 32 * 32;
   a.slab = slab;
   return a;
+}
+
+// Row-chunk wgrad launch (conv_wgrad_rows_kernel); returns the slab count, -1 on error.
+// R = output rows per chunk (ABD_WGRAD_R<layer> overrides, for tuning); the grid is the
+// resident block count (occupancy API) capped by the slab buffer.
+template <int NB, int CIN>
+int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int R,
+                      int max_slabs, float* slab, int phase, hipStream_t s) {
+  WGArgs a{};
+  a.dz = dz;
+  a.src = src;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.R = std::max(1, std::min(R, Ho));
+  a.cpb = (Ho + a.R - 1) / a.R;
+  a.nchunks = (int)(B * a.cpb);
+  a.dsz = (a.R * Wo * NB + 3) & ~3;
+  a.bsz = (a.dsz + (a.R + 1) * Ws * CIN + 3) & ~3;
+  a.slab = slab;
+  const size_t lds = 2 * (size_t)a.bsz * sizeof(float);
+  auto* kern = &conv_wgrad_rows_kernel<NB, CIN>;
+  static size_t cached_lds = 0;
+  static int per_cu = 1, n_cu = 256;
+  if (cached_lds != lds) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    int dev = 0;
+    ABD_HIP(hipGetDevice(&dev));
+    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kT, lds));
+    per_cu = std::max(1, per_cu);
+    cached_lds = lds;
+  }
+  int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
+  a.per = (a.nchunks + grid - 1) / grid;
+  grid = (a.nchunks + a.per - 1) / a.per;
+  if (phase >= 0) abd::prof_begin(phase, s);
+  kern<<<grid, kT, lds, s>>>(a);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return grid;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
 }
 
 template <int NB, int EPI>
@@ -1231,7 +1474,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     pa.coef = w.coef + 64;
     pa.out = w.p2;
     abd::prof_begin(abd::PH_BN2_POOL, s);
-    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 64), kT, 0, s>>>(pa);
+    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 64 / 4), kT, 0, s>>>(pa);
     abd::prof_end(abd::PH_BN2_POOL, s);
     ABD_LAUNCH_CHECK();
   }
@@ -1253,7 +1496,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     pa.out = w.p3d;
     pa.drop = drop1;
     abd::prof_begin(abd::PH_BN3_POOL, s);
-    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 32), kT, 0, s>>>(pa);
+    bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 32 / 4), kT, 0, s>>>(pa);
     abd::prof_end(abd::PH_BN3_POOL, s);
     ABD_LAUNCH_CHECK();
   }
@@ -1378,7 +1621,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.coef = w.coef + 128;
     pa.dp = w.dp3;
     pa.part = w.part;
-    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32);
+    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32 / 4);
     bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
     ABD_LAUNCH_CHECK();
     bn_bwd_finalize_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128,
@@ -1386,20 +1629,16 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     pa.bcoef = w.bcoef + 128;
     pa.dz = w.dz3;
-    pa.nblk = grid_for(B * g.H3 * g.W3 * 32);
+    pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 32 / 4);
     abd::prof_begin(abd::PH_BN3_BWD, s);
-    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, G[P_C3B]);
     ABD_LAUNCH_CHECK();
-    TNArgs ta = conv_wgrad_args(w.dz3, 32, w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, kConv3Slabs, w.slab);
-    const int nsl = (ta.M + ta.mchunk - 1) / ta.mchunk;
-    abd::prof_begin(abd::PH_CONV3_WGRAD, s);
-    gemm_tn_kernel<32, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
-    abd::prof_end(abd::PH_CONV3_WGRAD, s);
-    ABD_LAUNCH_CHECK();
-    if (reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
+    const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 8),
+                                              kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s);
+    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)) return -1;
   }
@@ -1410,7 +1649,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.coef = w.coef + 64;
     pa.dp = w.dp2;
     pa.part = w.part;
-    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64);
+    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
     bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
     ABD_LAUNCH_CHECK();
     bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64,
@@ -1418,20 +1657,16 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     pa.bcoef = w.bcoef + 64;
     pa.dz = w.dz2;
-    pa.nblk = grid_for(B * g.H2 * g.W2 * 64);
+    pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 64 / 4);
     abd::prof_begin(abd::PH_BN2_BWD, s);
-    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, G[P_C2B]);
     ABD_LAUNCH_CHECK();
-    TNArgs ta = conv_wgrad_args(w.dz2, 64, w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, kConv2Slabs, w.slab);
-    const int nsl = (ta.M + ta.mchunk - 1) / ta.mchunk;
-    abd::prof_begin(abd::PH_CONV2_WGRAD, s);
-    gemm_tn_kernel<64, 256><<<dim3(nsl, 1, 1), kT, 0, s>>>(ta);
-    abd::prof_end(abd::PH_CONV2_WGRAD, s);
-    ABD_LAUNCH_CHECK();
-    if (reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
+    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, env_int("ABD_WGRAD_R2", 3),
+                                              kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s);
+    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)) return -1;
   }
@@ -1548,7 +1783,7 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   ABD_CHECK(net && a && a->x && a->labels && a->params && a->grads && a->running, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
   ABD_CHECK(B >= 2, ABD_E_INVALID, "train step needs batch >= 2 (BatchNorm), got %lld", (long long)B);
-  ABD_CHECK(B * net->g.H2 * net->g.W2 < (1LL << 31), ABD_E_INVALID, "batch too large");
+  ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
             workspace_bytes, w.bytes);
@@ -1583,6 +1818,7 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
   ABD_CHECK(net && a && a->x && a->params && a->running && a->logprobs_out, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
   ABD_CHECK(B >= (train_mode ? 2 : 1), ABD_E_INVALID, "bad batch %lld", (long long)B);
+  ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
             workspace_bytes, w.bytes);
@@ -1615,6 +1851,8 @@ int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dl
                           size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(net && a && a->x && a->params && a->grads && dlogprobs, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
+  ABD_CHECK(B >= 2, ABD_E_INVALID, "backward needs batch >= 2 (BatchNorm), got %lld", (long long)B);
+  ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1645,6 +1883,7 @@ int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* 
                       void* workspace, size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(net && x && params && running && logprobs, ABD_E_INVALID, "NULL argument");
   if (batch == 0) return ABD_OK;
+  ABD_CHECK(batch * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, batch, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
             workspace_bytes, w.bytes);

@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--n-train", type=int, default=8192, help="resident training clips per GPU")
     ap.add_argument("--cpu-sample", type=int, default=192, help="utterances for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo for 1-GPU rehearsal")
     args = ap.parse_args()
 
@@ -145,9 +146,13 @@ def main():
     tr = ResidentTrainer(cfg, waves, labels, model, opt, args.batch, trigger=ultrasonic_trigger(60, "mid", False),
                          seed=35, rank=rank, world=world)
 
-    # warmup (untimed); every libabd phase bracketed to find the dominant kernel
-    with L.PhaseProfiler(L.PHASES, max_records=64 * max(args.warmup, 1)) as wprof:
-        for _ in range(args.warmup):
+    # warmup (untimed), then a few more untimed steps with every libabd phase bracketed to
+    # find the dominant kernel in steady state
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    with L.PhaseProfiler(L.PHASES, max_records=64 * args.profile_steps) as wprof:
+        for _ in range(args.profile_steps):
             tr.step()
         torch.cuda.synchronize()
     phases_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in wprof.result.items()}
