@@ -828,25 +828,28 @@ __global__ void __launch_bounds__(kT) gemm_tn_kernel(TNArgs a) {
 
 // 2x2 convolution weight gradient by output-row chunks.
 //   dW[n][t*CIN + ci] = sum_m dz[m][n] * src[row(m) + tap t][ci]
-// A chunk is R consecutive output rows of one utterance: its dz rows (R*Wo*NB floats) and
-// the R+1 source rows the four taps read ((R+1)*Ws*CIN floats) are both contiguous in
-// NHWC, so they are copied into LDS with global_load_lds (no VGPR staging, no index
-// math) into one of two buffers while the block runs the MFMAs of the previous chunk.
-// The taps are then constant LDS offsets.  Each wave owns TPW 32x32 accumulator tiles of
-// one n-tile; each block sums a contiguous range of chunks into its slab, reduced later
-// in slab order (deterministic).
+// A chunk is R consecutive output rows of one utterance.  Its R+1 source rows
+// ((R+1)*Ws*CIN floats) are contiguous in NHWC and are copied into LDS as is; its dz rows
+// are copied row by row to a row stride of Ws (= Wo + 1) positions, leaving a pad
+// column that is zeroed once.  On that common grid the reduction index m' = hl*Ws + w
+// addresses both operands linearly (dz at m'*NB, tap t's source at (m' + dh*Ws + dw)*CIN),
+// so the MFMA loop is pure base + immediate LDS reads; the pad positions contribute
+// zero products (Ws/Wo extra MFMAs).  Copies use global_load_lds into one of two buffers
+// while the block runs the MFMAs of the previous chunk.  Each wave owns TPW 32x32
+// accumulator tiles of one n-tile; each block sums a contiguous range of chunks into its
+// slab, reduced later in slab order (deterministic).
 struct WGArgs {
   const float* dz;   // (B, Ho, Wo, NB)
-  const float* src;  // (B, Hs, Ws, CIN), Hs >= Ho + 1, Ws >= Wo + 1
+  const float* src;  // (B, Hs, Ws, CIN), Hs >= Ho + 1, Ws == Wo + 1
   int Ho, Wo, Hs, Ws;
   int R, cpb, nchunks, per;
   int dsz, bsz;      // LDS floats: dz part (16-B aligned) and one whole buffer
   float* slab;       // [gridDim.x][NB][4*CIN]
 };
 
+// n16 16-byte pieces from g to l, lane-linear: wave-instruction j of wave w copies pieces
+// (j*kT + w*64) .. +63 into the same offsets of l
 __device__ __forceinline__ void glds_copy(const float* g, float* l, int n16) {
-  // n16 16-byte pieces, lane-linear: wave-instruction j of wave w copies pieces
-  // (j*kT + w*64) .. +63 into the same offsets of l
   const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
   for (int i0 = 0; i0 < n16; i0 += kT) {
     const int i = i0 + wbase + lane;
@@ -857,13 +860,14 @@ __device__ __forceinline__ void glds_copy(const float* g, float* l, int n16) {
 }
 
 template <int NB, int CIN>
-__global__ void __launch_bounds__(kT) conv_wgrad_rows_kernel(WGArgs a) {
+__global__ void __launch_bounds__(kT, 4) conv_wgrad_rows_kernel(WGArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_wg[];
   constexpr int KT = 4 * CIN / 32, TILES = (NB / 32) * KT, TPW = TILES / 4;
   static_assert(TILES % 4 == 0 && KT % TPW == 0, "a wave's tiles must share one n-tile");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int half = lane >> 5, col = lane & 31;
   const int nt = (wave * TPW) / KT;
+  const int rowd = a.Wo * NB / 4;  // 16-byte pieces per dz row
   int boff[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -871,6 +875,10 @@ __global__ void __launch_bounds__(kT) conv_wgrad_rows_kernel(WGArgs a) {
     const int tap = kt / (CIN / 32), cb = kt % (CIN / 32);
     boff[i] = ((tap >> 1) * a.Ws + (tap & 1)) * CIN + cb * 32 + col;
   }
+  // zero both buffers once: dz pad columns stay zero (copies never touch them) and every
+  // LDS word a pad position can read is finite (0 * finite = 0)
+  for (int i = threadIdx.x; i < 2 * a.bsz; i += kT) lds_wg[i] = 0.0f;
+  __syncthreads();
   f32x16 acc[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i)
@@ -880,7 +888,8 @@ __global__ void __launch_bounds__(kT) conv_wgrad_rows_kernel(WGArgs a) {
   auto stage = [&](int c, float* buf) {
     const int b = c / a.cpb, h0 = (c - b * a.cpb) * a.R;
     const int rows = min(a.R, a.Ho - h0);
-    glds_copy(a.dz + ((int64_t)b * a.Ho + h0) * a.Wo * NB, buf, rows * a.Wo * NB / 4);
+    const float* g = a.dz + ((int64_t)b * a.Ho + h0) * a.Wo * NB;
+    for (int r = 0; r < rows; ++r) glds_copy(g + r * a.Wo * NB, buf + r * a.Ws * NB, rowd);
     glds_copy(a.src + ((int64_t)b * a.Hs + h0) * a.Ws * CIN, buf + a.dsz, (rows + 1) * a.Ws * CIN / 4);
   };
   if (c0 < c1) stage(c0, lds_wg);
@@ -889,20 +898,27 @@ __global__ void __launch_bounds__(kT) conv_wgrad_rows_kernel(WGArgs a) {
     __syncthreads();  // chunk c landed (vmcnt(0) + barrier); the other buffer is free
     if (c + 1 < c1) stage(c + 1, lds_wg + ((c + 1 - c0) & 1) * a.bsz);
     const int h0 = (c % a.cpb) * a.R;
-    const int mcount = min(a.R, a.Ho - h0) * a.Wo;
-    const float* D = cur + nt * 32 + col;
-    const float* S = cur + a.dsz;
-    for (int mp = 0; mp < mcount; mp += 2) {
-      const int m = mp + half;
-      const bool ok = m < mcount;
-      const int hl = m / a.Wo, w = m - hl * a.Wo;
-      const float av = ok ? D[m * NB] : 0.0f;
-      const float* sp = S + (hl * a.Ws + w) * CIN;
+    const int rows = min(a.R, a.Ho - h0);
+    // m' over the rows*Ws grid positions in pairs; an odd count leaves out only the last
+    // position, which is a pad column (zero dz)
+    const int mcount = (rows * a.Ws) & ~1;
+    const float* D = cur + half * NB + nt * 32 + col;
+    const float* S = cur + a.dsz + half * CIN;
+    // software-pipelined one pair ahead (the read past the end lands in slack / zeros)
+    float av = D[0];
+    float bv[TPW];
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        const float bv = ok ? sp[boff[i]] : 0.0f;
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i], 0, 0, 0);
-      }
+    for (int i = 0; i < TPW; ++i) bv[i] = S[boff[i]];
+    for (int mp = 0; mp < mcount; mp += 2) {
+      const float avn = D[(mp + 2) * NB];
+      float bvn[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) bvn[i] = S[(mp + 2) * CIN + boff[i]];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[i], acc[i], 0, 0, 0);
+      av = avn;
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) bv[i] = bvn[i];
     }
   }
   float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
@@ -1346,6 +1362,7 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 template <int NB, int CIN>
 int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int R,
                       int max_slabs, float* slab, int phase, hipStream_t s) {
+  ABD_CHECK(Ws == Wo + 1 && Hs >= Ho + 1, ABD_E_UNSUPPORTED, "wgrad geometry");
   WGArgs a{};
   a.dz = dz;
   a.src = src;
@@ -1356,8 +1373,10 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
   a.R = std::max(1, std::min(R, Ho));
   a.cpb = (Ho + a.R - 1) / a.R;
   a.nchunks = (int)(B * a.cpb);
-  a.dsz = (a.R * Wo * NB + 3) & ~3;
-  a.bsz = (a.dsz + (a.R + 1) * Ws * CIN + 3) & ~3;
+  // dz on the Ws-strided grid; source rows + one slack row (a pad position's dh = 1 tap
+  // reads one row past the chunk)
+  a.dsz = ((a.R * Ws + 2) * NB + 3) & ~3;  // + 2 positions for the one-ahead read
+  a.bsz = (a.dsz + (a.R + 2) * Ws * CIN + 3) & ~3;
   a.slab = slab;
   const size_t lds = 2 * (size_t)a.bsz * sizeof(float);
   auto* kern = &conv_wgrad_rows_kernel<NB, CIN>;
@@ -1636,7 +1655,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, G[P_C3B]);
     ABD_LAUNCH_CHECK();
-    const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 8),
+    const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
                                               kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s);
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
@@ -1664,7 +1683,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, G[P_C2B]);
     ABD_LAUNCH_CHECK();
-    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, env_int("ABD_WGRAD_R2", 3),
+    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, env_int("ABD_WGRAD_R2", 1),
                                               kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s);
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
