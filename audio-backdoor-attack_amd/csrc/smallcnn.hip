@@ -31,7 +31,7 @@ using abd::kWave;
 constexpr float kEps = 1e-5f;
 constexpr float kMomentum = 0.1f;
 constexpr float kP1 = 0.4f, kP2 = 0.5f;
-constexpr int kR1 = 4;  // conv1 rows per block
+constexpr int kR1 = 8;  // conv1 rows per block
 
 struct Geo {
   int H0, W0, K, H1, W1, W1p, H2, W2, H2p, W2p, H3, W3, H3p, W3p, flat;
@@ -115,17 +115,39 @@ __device__ __forceinline__ void channel_partials(float (&v)[NV], int C, float* p
   }
 }
 
+// per-channel partial sums of NV values over the threads sharing a channel group
+// (thread t holds channels CPT*(t % CG) .. +CPT-1, CG = C/CPT); part[(j*C + c)*nblk + blk]
+template <int NV, int CPT = 4>
+__device__ __forceinline__ void cgroup_partials(float (&v)[NV][CPT], int C, float* part, int nblk, int blk) {
+  __shared__ float red[NV * CPT][kT];
+  const int t = threadIdx.x, CG = C / CPT;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) red[j * CPT + q][t] = v[j][q];
+  __syncthreads();
+  for (int o = t; o < NV * C; o += kT) {
+    const int j = o / C, c = o - j * C;
+    const int cg = c / CPT, q = c % CPT;
+    float sacc = 0.0f;
+    for (int u = cg; u < kT; u += CG) sacc += red[j * CPT + q][u];
+    part[((int64_t)j * C + c) * nblk + blk] = sacc;
+  }
+}
+
 // ------------------------------------------------------------------ conv1 (VALU, recomputed)
 // BatchNorm backward per-channel coefficients kept in double: dx = g * (dy - mdy - xhat * mdyx).
 // The batch means are subtracted from every element and the later weight-gradient sums
 // cancel 200-5000x, so rounding mdy / mdyx to fp32 would bias every element the same way.
+// With g = gamma*invstd, mdy = mean(dy), mdyx = mean(dy*xhat), xhat = (r - mean)*invstd:
+//   dx = g*(dy - mdy - xhat*mdyx) = g*dy + A + B*r,  A = g*(mdyx*invstd*mean - mdy),  B = -g*mdyx*invstd
+// evaluated as two double fmas.
 struct BCoef {
-  double g, mdy, mdyx, pad;
+  double g, A, B, pad;
 };
 
-__device__ __forceinline__ float bn_dx(float dy, float r, float4 cf, const BCoef& bc) {
-  const double xh = ((double)r - (double)cf.x) * (double)cf.y;
-  return (float)(((double)dy - bc.mdy - xh * bc.mdyx) * bc.g);
+__device__ __forceinline__ float bn_dx(float dy, float r, float4 /*cf*/, const BCoef& bc) {
+  return (float)fma(bc.B, (double)r, fma(bc.g, (double)dy, bc.A));
 }
 
 struct C1Args {
@@ -150,16 +172,51 @@ __device__ __forceinline__ void stage_x(const C1Args& a, int b, int h0, float* x
   __syncthreads();
 }
 
-__device__ __forceinline__ float conv1_at(const float* xs, int W0, int hl, int w, float w00, float w01, float w10,
-                                          float w11, float bias) {
+// conv1 kernels: one block per (utterance, kR1 rows); thread t owns channels 4*(t%16)..+3
+// (float4 weights / BN coefficients / NHWC stores) and walks positions or pool windows
+// t/16, t/16 + 16, ...  The x patch is read from LDS (broadcast across the 16 channel
+// groups).
+struct C1W {
+  float4 w00, w01, w10, w11, b;  // per-channel taps (kh,kw) and bias, 4 channels
+};
+
+__device__ __forceinline__ C1W c1_weights(const C1Args& a, int c0) {
+  C1W r;
+  float t[4][5];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[q][k] = a.w[(c0 + q) * 4 + k];
+    t[q][4] = a.b[c0 + q];
+  }
+  r.w00 = make_float4(t[0][0], t[1][0], t[2][0], t[3][0]);
+  r.w01 = make_float4(t[0][1], t[1][1], t[2][1], t[3][1]);
+  r.w10 = make_float4(t[0][2], t[1][2], t[2][2], t[3][2]);
+  r.w11 = make_float4(t[0][3], t[1][3], t[2][3], t[3][3]);
+  r.b = make_float4(t[0][4], t[1][4], t[2][4], t[3][4]);
+  return r;
+}
+
+// relu(conv1) at (hl, w) for 4 channels; same fma order as the oracle replay (b, w00, w01, w10, w11)
+__device__ __forceinline__ float4 c1_at(const float* xs, int W0, int hl, int w, const C1W& k) {
   const float* r0 = xs + hl * W0 + w;
-  const float* r1 = r0 + W0;
-  float v = bias;
-  v = fmaf(w00, r0[0], v);
-  v = fmaf(w01, r0[1], v);
-  v = fmaf(w10, r1[0], v);
-  v = fmaf(w11, r1[1], v);
-  return fmaxf(v, 0.0f);
+  const float x00 = r0[0], x01 = r0[1], x10 = r0[W0], x11 = r0[W0 + 1];
+  float4 v;
+  v.x = fmaxf(fmaf(k.w11.x, x11, fmaf(k.w10.x, x10, fmaf(k.w01.x, x01, fmaf(k.w00.x, x00, k.b.x)))), 0.0f);
+  v.y = fmaxf(fmaf(k.w11.y, x11, fmaf(k.w10.y, x10, fmaf(k.w01.y, x01, fmaf(k.w00.y, x00, k.b.y)))), 0.0f);
+  v.z = fmaxf(fmaf(k.w11.z, x11, fmaf(k.w10.z, x10, fmaf(k.w01.z, x01, fmaf(k.w00.z, x00, k.b.z)))), 0.0f);
+  v.w = fmaxf(fmaf(k.w11.w, x11, fmaf(k.w10.w, x10, fmaf(k.w01.w, x01, fmaf(k.w00.w, x00, k.b.w)))), 0.0f);
+  return v;
+}
+
+__device__ __forceinline__ float4 c1_coef_col(const float4* coef, int c0, int comp) {
+  float v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 cf = coef[c0 + q];
+    v[q] = comp == 0 ? cf.x : comp == 1 ? cf.y : comp == 2 ? cf.z : cf.w;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // forward stats: sum / sumsq of relu(conv1) per channel
@@ -168,20 +225,28 @@ __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
   const int nbh = (a.g.H1 + kR1 - 1) / kR1;
   const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
   stage_x(a, b, h0, xs);
-  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
-  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
+  const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
+  const C1W k = c1_weights(a, c0);
   const int rows = min(kR1, a.g.H1 - h0);
-  float v[2] = {0.0f, 0.0f};
-  for (int p = sub; p < rows * a.g.W1; p += 4) {
-    const int hl = p / a.g.W1, w = p - hl * a.g.W1;
-    const float r = conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb);
-    v[0] += r;
-    v[1] = fmaf(r, r, v[1]);
+  float v[2][4] = {};
+  for (int idx = pl; idx < rows * a.g.W1; idx += 16) {
+    const int hl = idx / a.g.W1, w = idx - hl * a.g.W1;
+    const float4 r = c1_at(xs, a.g.W0, hl, w, k);
+    v[0][0] += r.x;
+    v[0][1] += r.y;
+    v[0][2] += r.z;
+    v[0][3] += r.w;
+    v[1][0] = fmaf(r.x, r.x, v[1][0]);
+    v[1][1] = fmaf(r.y, r.y, v[1][1]);
+    v[1][2] = fmaf(r.z, r.z, v[1][2]);
+    v[1][3] = fmaf(r.w, r.w, v[1][3]);
   }
-  channel_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
+  cgroup_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
 }
 
-__device__ __forceinline__ int argmax3(float y0, float y1, float y2, float& best) {
+// first maximum of bn(r) over a (1,3) window, per channel: returns the slot index 0..2
+__device__ __forceinline__ int c1_argmax(float r0, float r1, float r2, float al, float be, float& best) {
+  const float y0 = fmaf(al, r0, be), y1 = fmaf(al, r1, be), y2 = fmaf(al, r2, be);
   int j = 0;
   best = y0;
   if (y1 > best) {
@@ -201,19 +266,22 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
   const int nbh = (a.g.H1 + kR1 - 1) / kR1;
   const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
   stage_x(a, b, h0, xs);
-  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
-  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
-  const float4 cf = a.coef[c];
+  const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
+  const C1W k = c1_weights(a, c0);
+  const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
   const int rows = min(kR1, a.g.H1 - h0);
-  for (int p = sub; p < rows * a.g.W1p; p += 4) {
-    const int hl = p / a.g.W1p, wo = p - hl * a.g.W1p;
+  const int NW = a.g.W1p;
+  for (int idx = pl; idx < rows * NW; idx += 16) {
+    const int hl = idx / NW, wo = idx - hl * NW;
     const int w = 3 * wo;
-    const float y0 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb), cf.w);
-    const float y1 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w + 1, w00, w01, w10, w11, bb), cf.w);
-    const float y2 = fmaf(cf.z, conv1_at(xs, a.g.W0, hl, w + 2, w00, w01, w10, w11, bb), cf.w);
-    float best;
-    argmax3(y0, y1, y2, best);
-    a.p1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c] = best;
+    const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
+                 r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
+    float4 o;
+    c1_argmax(r0.x, r1.x, r2.x, al.x, be.x, o.x);
+    c1_argmax(r0.y, r1.y, r2.y, al.y, be.y, o.y);
+    c1_argmax(r0.z, r1.z, r2.z, al.z, be.z, o.z);
+    c1_argmax(r0.w, r1.w, r2.w, al.w, be.w, o.w);
+    *reinterpret_cast<float4*>(a.p1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0) = o;
   }
 }
 
@@ -223,71 +291,103 @@ __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
   const int nbh = (a.g.H1 + kR1 - 1) / kR1;
   const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
   stage_x(a, b, h0, xs);
-  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
-  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
-  const float4 cf = a.coef[c];
+  const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
+  const C1W k = c1_weights(a, c0);
+  const float4 mu = c1_coef_col(a.coef, c0, 0), is = c1_coef_col(a.coef, c0, 1);
+  const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
   const int rows = min(kR1, a.g.H1 - h0);
-  float v[2] = {0.0f, 0.0f};
-  for (int p = sub; p < rows * a.g.W1p; p += 4) {
-    const int hl = p / a.g.W1p, wo = p - hl * a.g.W1p;
+  const int NW = a.g.W1p;
+  float v[2][4] = {};
+  for (int idx = pl; idx < rows * NW; idx += 16) {
+    const int hl = idx / NW, wo = idx - hl * NW;
     const int w = 3 * wo;
-    const float r0 = conv1_at(xs, a.g.W0, hl, w, w00, w01, w10, w11, bb);
-    const float r1 = conv1_at(xs, a.g.W0, hl, w + 1, w00, w01, w10, w11, bb);
-    const float r2 = conv1_at(xs, a.g.W0, hl, w + 2, w00, w01, w10, w11, bb);
-    float best;
-    const int j = argmax3(fmaf(cf.z, r0, cf.w), fmaf(cf.z, r1, cf.w), fmaf(cf.z, r2, cf.w), best);
-    const float rs = j == 0 ? r0 : (j == 1 ? r1 : r2);
-    const float dy = a.dp1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c];
-    v[0] += dy;
-    v[1] = fmaf(dy, (rs - cf.x) * cf.y, v[1]);
+    const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
+                 r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
+    const float4 dy = *reinterpret_cast<const float4*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0);
+    const float rr0[4] = {r0.x, r0.y, r0.z, r0.w}, rr1[4] = {r1.x, r1.y, r1.z, r1.w}, rr2[4] = {r2.x, r2.y, r2.z, r2.w};
+    const float aa[4] = {al.x, al.y, al.z, al.w}, bb[4] = {be.x, be.y, be.z, be.w};
+    const float mm[4] = {mu.x, mu.y, mu.z, mu.w}, ii[4] = {is.x, is.y, is.z, is.w};
+    const float dd[4] = {dy.x, dy.y, dy.z, dy.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float best;
+      const int j = c1_argmax(rr0[q], rr1[q], rr2[q], aa[q], bb[q], best);
+      const float rs = j == 0 ? rr0[q] : (j == 1 ? rr1[q] : rr2[q]);
+      v[0][q] += dd[q];
+      v[1][q] = fmaf(dd[q], (rs - mm[q]) * ii[q], v[1][q]);
+    }
   }
-  channel_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
+  cgroup_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
 }
 
-// backward: BN1 dx -> relu mask -> conv1 weight / bias gradient partials (5 per channel)
+// backward: BN1 dx -> relu mask -> conv1 weight / bias gradient partials (5 per channel).
+// 2 channels per thread (the double-precision BN coefficients would otherwise cap occupancy).
 __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
   __shared__ float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + kR1 - 1) / kR1;
   const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
   stage_x(a, b, h0, xs);
-  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
-  const float w00 = a.w[c * 4 + 0], w01 = a.w[c * 4 + 1], w10 = a.w[c * 4 + 2], w11 = a.w[c * 4 + 3], bb = a.b[c];
-  const float4 cf = a.coef[c];
-  const BCoef bc = a.bcoef[c];
+  constexpr int CPT = 2;
+  const int c0 = (threadIdx.x & 31) * CPT, pl = threadIdx.x >> 5;
+  float kw[CPT][5], aa[CPT], bb[CPT];
+  BCoef bc[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kw[q][t] = a.w[(c0 + q) * 4 + t];
+    kw[q][4] = a.b[c0 + q];
+    const float4 cf = a.coef[c0 + q];
+    aa[q] = cf.z;
+    bb[q] = cf.w;
+    bc[q] = a.bcoef[c0 + q];
+  }
   const int rows = min(kR1, a.g.H1 - h0);
-  const int nwin = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
-  float v[5] = {0, 0, 0, 0, 0};
-  for (int p = sub; p < rows * nwin; p += 4) {
-    const int hl = p / nwin, wo = p - hl * nwin;
+  const int NW = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
+  float v[5][CPT] = {};
+  for (int idx = pl; idx < rows * NW; idx += kT / 32) {
+    const int hl = idx / NW, wo = idx - hl * NW;
     const int w = 3 * wo;
     const int nw = min(3, a.g.W1 - w);
-    float r[3], y[3];
+    const bool real = wo < a.g.W1p;
+    const float* x0 = xs + hl * a.g.W0 + w;
+    float xv[2][4];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      r[j] = (j < nw) ? conv1_at(xs, a.g.W0, hl, w + j, w00, w01, w10, w11, bb) : 0.0f;
-      y[j] = fmaf(cf.z, r[j], cf.w);
+    for (int j = 0; j < 4; ++j) {
+      xv[0][j] = (j <= nw) ? x0[j] : 0.0f;
+      xv[1][j] = (j <= nw) ? x0[a.g.W0 + j] : 0.0f;
     }
-    int jm = -1;
-    float dyv = 0.0f;
-    if (wo < a.g.W1p) {
+    float dd[CPT];
+    if (real) {
+      const float2 d2 = *reinterpret_cast<const float2*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c0);
+      dd[0] = d2.x;
+      dd[1] = d2.y;
+    } else {
+      dd[0] = dd[1] = 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      float r[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)  // same fma order as the oracle replay (b, w00, w01, w10, w11)
+        r[j] = (j < nw) ? fmaxf(fmaf(kw[q][3], xv[1][j + 1], fmaf(kw[q][2], xv[1][j], fmaf(kw[q][1], xv[0][j + 1],
+                                                                                          fmaf(kw[q][0], xv[0][j], kw[q][4])))),
+                                0.0f)
+                        : 0.0f;
       float best;
-      jm = argmax3(y[0], y[1], y[2], best);
-      dyv = a.dp1[(((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c];
-    }
+      const int jm = real ? c1_argmax(r[0], r[1], r[2], aa[q], bb[q], best) : -1;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (j >= nw) continue;
-      const float dy = (j == jm) ? dyv : 0.0f;
-      const float dz = r[j] > 0.0f ? bn_dx(dy, r[j], cf, bc) : 0.0f;
-      const float* x0 = xs + hl * a.g.W0 + w + j;
-      v[0] = fmaf(dz, x0[0], v[0]);
-      v[1] = fmaf(dz, x0[1], v[1]);
-      v[2] = fmaf(dz, x0[a.g.W0], v[2]);
-      v[3] = fmaf(dz, x0[a.g.W0 + 1], v[3]);
-      v[4] += dz;
+      for (int j = 0; j < 3; ++j) {
+        if (j >= nw) continue;
+        const float dz = r[j] > 0.0f ? bn_dx(j == jm ? dd[q] : 0.0f, r[j], float4{}, bc[q]) : 0.0f;
+        v[0][q] = fmaf(dz, xv[0][j], v[0][q]);
+        v[1][q] = fmaf(dz, xv[0][j + 1], v[1][q]);
+        v[2][q] = fmaf(dz, xv[1][j], v[2][q]);
+        v[3][q] = fmaf(dz, xv[1][j + 1], v[3][q]);
+        v[4][q] += dz;
+      }
     }
   }
-  channel_partials<5>(v, 64, a.part, a.nblk, blockIdx.x);
+  cgroup_partials<5, CPT>(v, 64, a.part, a.nblk, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ BN statistics
@@ -359,7 +459,9 @@ __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, 
     s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     dgamma[c] = (float)s2;
     dbeta[c] = (float)s1;
-    bcoef[c] = BCoef{(double)gamma[c] * (double)coef[c].y, s1 / count, s2 / count, 0.0};
+    const double g = (double)gamma[c] * (double)coef[c].y, mdy = s1 / count, mdyx = s2 / count;
+    const double mean = (double)coef[c].x, invstd = (double)coef[c].y;
+    bcoef[c] = BCoef{g, g * (mdyx * invstd * mean - mdy), -g * mdyx * invstd, 0.0};
   }
 }
 
@@ -454,26 +556,6 @@ __device__ __forceinline__ void win_argmax(const PoolArgs& a, int b, int ho, int
 __device__ __forceinline__ int pooled_index(const PoolArgs& a, int b, int ho, int wo, int c) {
   if (a.flat_n > 0) return b * a.flat_n + (c * a.Ho + ho) * a.Wo + wo;
   return ((b * a.Ho + ho) * a.Wo + wo) * a.C + c;
-}
-
-// per-channel partial sums of NV values over the threads sharing a channel group
-// (thread t holds channels 4*(t % CG) .. +3); part[(j*C + c)*nblk + blk]
-template <int NV>
-__device__ __forceinline__ void cgroup_partials(float (&v)[NV][4], int C, float* part, int nblk, int blk) {
-  __shared__ float red[NV * 4][kT];
-  const int t = threadIdx.x, CG = C / 4;
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) red[j * 4 + q][t] = v[j][q];
-  __syncthreads();
-  for (int o = t; o < NV * C; o += kT) {
-    const int j = o / C, c = o - j * C;
-    const int cg = c / 4, q = c % 4;
-    float sacc = 0.0f;
-    for (int u = cg; u < kT; u += CG) sacc += red[j * 4 + q][u];
-    part[((int64_t)j * C + c) * nblk + blk] = sacc;
-  }
 }
 
 __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
