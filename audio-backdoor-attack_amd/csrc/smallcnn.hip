@@ -31,7 +31,7 @@ using abd::kWave;
 constexpr float kEps = 1e-5f;
 constexpr float kMomentum = 0.1f;
 constexpr float kP1 = 0.4f, kP2 = 0.5f;
-constexpr int kR1 = 8;  // conv1 rows per block
+constexpr int kR1 = 8;  // max conv1 rows per chunk (LDS staging size); C1Args::rows is the actual
 
 struct Geo {
   int H0, W0, K, H1, W1, W1p, H2, W2, H2p, W2p, H3, W3, H3p, W3p, flat;
@@ -162,11 +162,12 @@ struct C1Args {
   int nblk;
   Geo g;
   int B;
+  int rows;  // conv1 rows per chunk (<= kR1)
 };
 
 // Stage x rows [h0, h0+kR1] of utterance b into LDS.
 __device__ __forceinline__ void stage_x(const C1Args& a, int b, int h0, float* xs) {
-  const int rows = min(kR1 + 1, a.g.H0 - h0);
+  const int rows = min(a.rows + 1, a.g.H0 - h0);
   const float* src = a.x + ((int64_t)b * a.g.H0 + h0) * a.g.W0;
   for (int i = threadIdx.x; i < rows * a.g.W0; i += kT) xs[i] = src[i];
   __syncthreads();
@@ -222,24 +223,28 @@ __device__ __forceinline__ float4 c1_coef_col(const float4* coef, int c0, int co
 // forward stats: sum / sumsq of relu(conv1) per channel
 __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
   __shared__ float xs[(kR1 + 1) * 128];
-  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
-  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
-  stage_x(a, b, h0, xs);
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
   const C1W k = c1_weights(a, c0);
-  const int rows = min(kR1, a.g.H1 - h0);
   float v[2][4] = {};
-  for (int idx = pl; idx < rows * a.g.W1; idx += 16) {
-    const int hl = idx / a.g.W1, w = idx - hl * a.g.W1;
-    const float4 r = c1_at(xs, a.g.W0, hl, w, k);
-    v[0][0] += r.x;
-    v[0][1] += r.y;
-    v[0][2] += r.z;
-    v[0][3] += r.w;
-    v[1][0] = fmaf(r.x, r.x, v[1][0]);
-    v[1][1] = fmaf(r.y, r.y, v[1][1]);
-    v[1][2] = fmaf(r.z, r.z, v[1][2]);
-    v[1][3] = fmaf(r.w, r.w, v[1][3]);
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    for (int idx = pl; idx < rows * a.g.W1; idx += 16) {
+      const int hl = idx / a.g.W1, w = idx - hl * a.g.W1;
+      const float4 r = c1_at(xs, a.g.W0, hl, w, k);
+      v[0][0] += r.x;
+      v[0][1] += r.y;
+      v[0][2] += r.z;
+      v[0][3] += r.w;
+      v[1][0] = fmaf(r.x, r.x, v[1][0]);
+      v[1][1] = fmaf(r.y, r.y, v[1][1]);
+      v[1][2] = fmaf(r.z, r.z, v[1][2]);
+      v[1][3] = fmaf(r.w, r.w, v[1][3]);
+    }
+    __syncthreads();  // xs is restaged by the next chunk
   }
   cgroup_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
 }
@@ -263,59 +268,67 @@ __device__ __forceinline__ int c1_argmax(float r0, float r1, float r2, float al,
 // forward: relu(conv1) -> BN1 -> maxpool(1,3) -> p1 (NHWC)
 __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
   __shared__ float xs[(kR1 + 1) * 128];
-  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
-  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
-  stage_x(a, b, h0, xs);
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
   const C1W k = c1_weights(a, c0);
   const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
-  const int rows = min(kR1, a.g.H1 - h0);
   const int NW = a.g.W1p;
-  for (int idx = pl; idx < rows * NW; idx += 16) {
-    const int hl = idx / NW, wo = idx - hl * NW;
-    const int w = 3 * wo;
-    const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
-                 r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
-    float4 o;
-    c1_argmax(r0.x, r1.x, r2.x, al.x, be.x, o.x);
-    c1_argmax(r0.y, r1.y, r2.y, al.y, be.y, o.y);
-    c1_argmax(r0.z, r1.z, r2.z, al.z, be.z, o.z);
-    c1_argmax(r0.w, r1.w, r2.w, al.w, be.w, o.w);
-    *reinterpret_cast<float4*>(a.p1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0) = o;
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    for (int idx = pl; idx < rows * NW; idx += 16) {
+      const int hl = idx / NW, wo = idx - hl * NW;
+      const int w = 3 * wo;
+      const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
+                   r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
+      float4 o;
+      c1_argmax(r0.x, r1.x, r2.x, al.x, be.x, o.x);
+      c1_argmax(r0.y, r1.y, r2.y, al.y, be.y, o.y);
+      c1_argmax(r0.z, r1.z, r2.z, al.z, be.z, o.z);
+      c1_argmax(r0.w, r1.w, r2.w, al.w, be.w, o.w);
+      *reinterpret_cast<float4*>(a.p1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0) = o;
+    }
+    __syncthreads();  // xs is restaged by the next chunk
   }
 }
 
 // backward stats: s1 = sum dy, s2 = sum dy * xhat over pool1 argmax positions
 __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
   __shared__ float xs[(kR1 + 1) * 128];
-  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
-  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
-  stage_x(a, b, h0, xs);
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
   const C1W k = c1_weights(a, c0);
   const float4 mu = c1_coef_col(a.coef, c0, 0), is = c1_coef_col(a.coef, c0, 1);
   const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
-  const int rows = min(kR1, a.g.H1 - h0);
   const int NW = a.g.W1p;
   float v[2][4] = {};
-  for (int idx = pl; idx < rows * NW; idx += 16) {
-    const int hl = idx / NW, wo = idx - hl * NW;
-    const int w = 3 * wo;
-    const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
-                 r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
-    const float4 dy = *reinterpret_cast<const float4*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0);
-    const float rr0[4] = {r0.x, r0.y, r0.z, r0.w}, rr1[4] = {r1.x, r1.y, r1.z, r1.w}, rr2[4] = {r2.x, r2.y, r2.z, r2.w};
-    const float aa[4] = {al.x, al.y, al.z, al.w}, bb[4] = {be.x, be.y, be.z, be.w};
-    const float mm[4] = {mu.x, mu.y, mu.z, mu.w}, ii[4] = {is.x, is.y, is.z, is.w};
-    const float dd[4] = {dy.x, dy.y, dy.z, dy.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float best;
-      const int j = c1_argmax(rr0[q], rr1[q], rr2[q], aa[q], bb[q], best);
-      const float rs = j == 0 ? rr0[q] : (j == 1 ? rr1[q] : rr2[q]);
-      v[0][q] += dd[q];
-      v[1][q] = fmaf(dd[q], (rs - mm[q]) * ii[q], v[1][q]);
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    for (int idx = pl; idx < rows * NW; idx += 16) {
+      const int hl = idx / NW, wo = idx - hl * NW;
+      const int w = 3 * wo;
+      const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
+                   r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
+      const float4 dy = *reinterpret_cast<const float4*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * NW + wo) * 64 + c0);
+      const float rr0[4] = {r0.x, r0.y, r0.z, r0.w}, rr1[4] = {r1.x, r1.y, r1.z, r1.w}, rr2[4] = {r2.x, r2.y, r2.z, r2.w};
+      const float aa[4] = {al.x, al.y, al.z, al.w}, bb[4] = {be.x, be.y, be.z, be.w};
+      const float mm[4] = {mu.x, mu.y, mu.z, mu.w}, ii[4] = {is.x, is.y, is.z, is.w};
+      const float dd[4] = {dy.x, dy.y, dy.z, dy.w};
+  #pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float best;
+        const int j = c1_argmax(rr0[q], rr1[q], rr2[q], aa[q], bb[q], best);
+        const float rs = j == 0 ? rr0[q] : (j == 1 ? rr1[q] : rr2[q]);
+        v[0][q] += dd[q];
+        v[1][q] = fmaf(dd[q], (rs - mm[q]) * ii[q], v[1][q]);
+      }
     }
+    __syncthreads();  // xs is restaged by the next chunk
   }
   cgroup_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
 }
@@ -324,9 +337,8 @@ __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
 // 2 channels per thread (the double-precision BN coefficients would otherwise cap occupancy).
 __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
   __shared__ float xs[(kR1 + 1) * 128];
-  const int nbh = (a.g.H1 + kR1 - 1) / kR1;
-  const int b = blockIdx.x / nbh, h0 = (blockIdx.x % nbh) * kR1;
-  stage_x(a, b, h0, xs);
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int nchunks = a.B * nbh;
   constexpr int CPT = 2;
   const int c0 = (threadIdx.x & 31) * CPT, pl = threadIdx.x >> 5;
   float kw[CPT][5], aa[CPT], bb[CPT];
@@ -341,61 +353,68 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     bb[q] = cf.w;
     bc[q] = a.bcoef[c0 + q];
   }
-  const int rows = min(kR1, a.g.H1 - h0);
   const int NW = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
   float v[5][CPT] = {};
-  for (int idx = pl; idx < rows * NW; idx += kT / 32) {
-    const int hl = idx / NW, wo = idx - hl * NW;
-    const int w = 3 * wo;
-    const int nw = min(3, a.g.W1 - w);
-    const bool real = wo < a.g.W1p;
-    const float* x0 = xs + hl * a.g.W0 + w;
-    float xv[2][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      xv[0][j] = (j <= nw) ? x0[j] : 0.0f;
-      xv[1][j] = (j <= nw) ? x0[a.g.W0 + j] : 0.0f;
-    }
-    float dd[CPT];
-    if (real) {
-      const float2 d2 = *reinterpret_cast<const float2*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c0);
-      dd[0] = d2.x;
-      dd[1] = d2.y;
-    } else {
-      dd[0] = dd[1] = 0.0f;
-    }
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      float r[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j)  // same fma order as the oracle replay (b, w00, w01, w10, w11)
-        r[j] = (j < nw) ? fmaxf(fmaf(kw[q][3], xv[1][j + 1], fmaf(kw[q][2], xv[1][j], fmaf(kw[q][1], xv[0][j + 1],
-                                                                                          fmaf(kw[q][0], xv[0][j], kw[q][4])))),
-                                0.0f)
-                        : 0.0f;
-      float best;
-      const int jm = real ? c1_argmax(r[0], r[1], r[2], aa[q], bb[q], best) : -1;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (j >= nw) continue;
-        const float dz = r[j] > 0.0f ? bn_dx(j == jm ? dd[q] : 0.0f, r[j], float4{}, bc[q]) : 0.0f;
-        v[0][q] = fmaf(dz, xv[0][j], v[0][q]);
-        v[1][q] = fmaf(dz, xv[0][j + 1], v[1][q]);
-        v[2][q] = fmaf(dz, xv[1][j], v[2][q]);
-        v[3][q] = fmaf(dz, xv[1][j + 1], v[3][q]);
-        v[4][q] += dz;
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    for (int idx = pl; idx < rows * NW; idx += kT / 32) {
+      const int hl = idx / NW, wo = idx - hl * NW;
+      const int w = 3 * wo;
+      const int nw = min(3, a.g.W1 - w);
+      const bool real = wo < a.g.W1p;
+      const float* x0 = xs + hl * a.g.W0 + w;
+      float xv[2][4];
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xv[0][j] = (j <= nw) ? x0[j] : 0.0f;
+        xv[1][j] = (j <= nw) ? x0[a.g.W0 + j] : 0.0f;
+      }
+      float dd[CPT];
+      if (real) {
+        const float2 d2 = *reinterpret_cast<const float2*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c0);
+        dd[0] = d2.x;
+        dd[1] = d2.y;
+      } else {
+        dd[0] = dd[1] = 0.0f;
+      }
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        float r[3];
+  #pragma unroll
+        for (int j = 0; j < 3; ++j)  // same fma order as the oracle replay (b, w00, w01, w10, w11)
+          r[j] = (j < nw) ? fmaxf(fmaf(kw[q][3], xv[1][j + 1], fmaf(kw[q][2], xv[1][j], fmaf(kw[q][1], xv[0][j + 1],
+                                                                                            fmaf(kw[q][0], xv[0][j], kw[q][4])))),
+                                  0.0f)
+                          : 0.0f;
+        float best;
+        const int jm = real ? c1_argmax(r[0], r[1], r[2], aa[q], bb[q], best) : -1;
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j >= nw) continue;
+          const float dz = r[j] > 0.0f ? bn_dx(j == jm ? dd[q] : 0.0f, r[j], float4{}, bc[q]) : 0.0f;
+          v[0][q] = fmaf(dz, xv[0][j], v[0][q]);
+          v[1][q] = fmaf(dz, xv[0][j + 1], v[1][q]);
+          v[2][q] = fmaf(dz, xv[1][j], v[2][q]);
+          v[3][q] = fmaf(dz, xv[1][j + 1], v[3][q]);
+          v[4][q] += dz;
+        }
       }
     }
+    __syncthreads();  // xs is restaged by the next chunk
   }
   cgroup_partials<5, CPT>(v, 64, a.part, a.nblk, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ BN statistics
 // part layout: [(j*C + c) * nblk + blk], j = 0 sum, 1 sumsq
+// nbt (optional): BatchNorm num_batches_tracked of all three layers, incremented once
 __global__ void __launch_bounds__(kT) bn_finalize_kernel(const float* part, int nblk, int C, double count,
                                                          const float* gamma, const float* beta, float* rm, float* rv,
-                                                         float4* coef) {
+                                                         float4* coef, int64_t* nbt = nullptr) {
   const int c = blockIdx.x;
+  if (nbt != nullptr && c == 0 && threadIdx.x < 3) nbt[threadIdx.x] += 1;
   double s = 0.0, ss = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) {
     s += part[(int64_t)c * nblk + i];
@@ -466,7 +485,9 @@ __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, 
 }
 
 // sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
-__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out) {
+// conv1 mode (gw != nullptr): columns j*64 + c, j < 4 -> conv1.weight (c,1,kh,kw) = gw[c*4 + j], j = 4 -> gb[c]
+__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out,
+                                                         float* gw = nullptr, float* gb = nullptr) {
   const int col = blockIdx.x;
   double s = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) s += part[(int64_t)col * nblk + i];
@@ -474,7 +495,12 @@ __global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int 
   s = abd::wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) out[col] = (float)(red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    const float v = (float)(red[0] + red[1] + red[2] + red[3]);
+    if (gw == nullptr) out[col] = v;
+    else if (col < 4 * 64) gw[(col % 64) * 4 + col / 64] = v;
+    else gb[col - 4 * 64] = v;
+  }
 }
 
 // ------------------------------------------------------------------ BN + max-pool (layers 2, 3)
@@ -685,19 +711,22 @@ struct NTArgs {
 
 constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
 
-template <int NB, int EPI>
+// MI = 32-row m-tiles per wave (block rows = 128 * MI): MI = 2 gives each wave a 2 x NJ
+// accumulator grid, one LDS read per MFMA instead of 1.5 for NB = 64.
+template <int NB, int EPI, int MI = 1>
 __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
-  __shared__ float As[kBM * kLDA];
+  constexpr int BM = kBM * MI, RPT = BM / 32;
+  __shared__ float As[BM * kLDA];
   __shared__ float Bs[NB * kLDA];
   constexpr int NJ = NB / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * kBM;
+  const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * NB;
   const int q4 = tid & 7;
-  int rb[4], rh[4], rw[4];
-  bool rok[4];
+  int rb[RPT], rh[RPT], rw[RPT];
+  bool rok[RPT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RPT; ++i) {
     const int m = m0 + (tid >> 3) + 32 * i;
     rok[i] = m < a.M;
     const int mm = rok[i] ? m : 0;
@@ -711,12 +740,12 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
   const int ch_begin = (int)((int64_t)nch_all * blockIdx.z / ks);
   const int nch = (int)((int64_t)nch_all * (blockIdx.z + 1) / ks);
-  float4 ra[4], rbv[NJ];
+  float4 ra[RPT], rbv[NJ];
   auto load = [&](int ch) {
     const int t = ch / cpt;
     const int c0 = (ch - t * cpt) * kKC;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RPT; ++i) {
       const int hs = rh[i] + a.dh[t], ws = rw[i] + a.dw[t];
       const bool ok = rok[i] && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws;
       ra[i] = ok ? *reinterpret_cast<const float4*>(a.src + (((int64_t)rb[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c0 +
@@ -731,16 +760,18 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  f32x16 acc[NJ];
+  f32x16 acc[MI][NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   load(ch_begin);
   for (int ch = ch_begin; ch < nch; ++ch) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RPT; ++i) {
       float* d = As + ((tid >> 3) + 32 * i) * kLDA + 4 * q4;
       d[0] = ra[i].x;
       d[1] = ra[i].y;
@@ -758,18 +789,24 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
     }
     __syncthreads();
     if (ch + 1 < nch) load(ch + 1);
-    const float* ap = As + (wave * 32 + (lane & 31)) * kLDA + (lane >> 5);
+    const float* ap = As + (wave * 32 * MI + (lane & 31)) * kLDA + (lane >> 5);
     const float* bp = Bs + (lane & 31) * kLDA + (lane >> 5);
 #pragma unroll
     for (int kk = 0; kk < kKC; kk += 2) {
-      const float av = ap[kk];
+      float av[MI];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bp[j * 32 * kLDA + kk], acc[j], 0, 0, 0);
+      for (int i = 0; i < MI; ++i) av[i] = ap[i * 32 * kLDA + kk];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float bv = bp[j * 32 * kLDA + kk];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv, acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
 
-  // epilogue: acc[j][r] -> row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31 of tile j
+  // epilogue: acc[i][j][r] -> row i*32 + (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32*MI, col lane&31 of tile j
   float st[NJ][2];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -780,10 +817,12 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
     float bias = 0.0f;
     if constexpr (EPI == EPI_CONV || EPI == EPI_FC1) bias = cok ? a.bias[col] : 0.0f;
 #pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int m = m0 + wave * 32 * MI + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= a.M || !cok) continue;
-      float v = acc[j][r];
+      float v = acc[i][j][r];
       int64_t oi = (int64_t)m * a.ldc + col;
       if constexpr (EPI == EPI_PARTIAL) oi += (int64_t)blockIdx.z * a.M * a.ldc;
       if constexpr (EPI == EPI_CONV) {
@@ -1251,10 +1290,6 @@ __global__ void __launch_bounds__(kT) logsoftmax_bwd_kernel(const float* dlp, co
   if (act) dz[(int64_t)row * K + lane] = d - expf(lp[(int64_t)row * K + lane]) * sd;
 }
 
-__global__ void inc_i64_kernel(int64_t* p, int n) {
-  if ((int)threadIdx.x < n) p[threadIdx.x] += 1;
-}
-
 int grid_for(int64_t total, int cap = 4096) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((total + kT - 1) / kT, cap));
 }
@@ -1286,7 +1321,15 @@ struct Work {
 constexpr int kConv2Slabs = 1024, kConv3Slabs = 1024, kFc1MSplit = 8, kFc1KSplit = 48, kFc2Split = 16;
 constexpr int kSlabGroup = 32;
 
-int64_t nblk_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + kR1 - 1) / kR1); }
+// conv1 kernels loop over (utterance, rows) chunks; the capped grid keeps the BN partial count small.
+// ABD_C1_ROWS / ABD_C1_CAP override (tuning).
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+int c1_rows() { return std::max(1, std::min(kR1, env_int("ABD_C1_ROWS", 8))); }
+int64_t nchunks_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + c1_rows() - 1) / c1_rows()); }
+int64_t nblk_conv1(const Geo& g, int64_t B) { return std::min<int64_t>(nchunks_conv1(g, B), env_int("ABD_C1_CAP", 2048)); }
 
 Work layout(const abd_cnn* net, int64_t B, char* base) {
   const Geo& g = net->g;
@@ -1484,16 +1527,12 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
   return grid;
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
 
-template <int NB, int EPI>
+template <int NB, int EPI, int MI = 1>
 int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
-  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
+  dim3 grid((a.M + kBM * MI - 1) / (kBM * MI), (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
   if (phase >= 0) abd::prof_begin(phase, s);
-  gemm_nt_kernel<NB, EPI><<<grid, dim3(kT), 0, s>>>(a);
+  gemm_nt_kernel<NB, EPI, MI><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -1518,7 +1557,8 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
 
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
-            float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s) {
+            float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
+            int64_t* nbt = nullptr) {
   const Geo& g = net->g;
   C1Args c1{};
   c1.x = x;
@@ -1530,6 +1570,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   c1.g = g;
   c1.B = (int)B;
   c1.nblk = (int)nblk_conv1(g, B);
+  c1.rows = c1_rows();
   const float* rm[3] = {running_in, running_in + 128, running_in + 256};
   const float* rv[3] = {running_in + 64, running_in + 192, running_in + 288};
   float* rmu[3] = {nullptr, nullptr, nullptr};
@@ -1549,13 +1590,13 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     abd::prof_end(abd::PH_CONV1_STATS, s);
     ABD_LAUNCH_CHECK();
     bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B],
-                                         rmu[0], rvu[0], w.coef);
+                                         rmu[0], rvu[0], w.coef, running_upd ? nbt : nullptr);
   } else {
     bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN1W], P.p[P_BN1B], rm[0], rv[0], 64, w.coef);
   }
   ABD_LAUNCH_CHECK();
   abd::prof_begin(abd::PH_CONV1_POOL, s);
-    conv1_bn_pool_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    conv1_bn_pool_kernel<<<(unsigned)nchunks_conv1(g, B), kT, 0, s>>>(c1);  // no partials: one chunk per block
     abd::prof_end(abd::PH_CONV1_POOL, s);
   ABD_LAUNCH_CHECK();
   // ---- layer 2: conv2 (MFMA) + relu + stats -> BN2 -> pool2
@@ -1783,6 +1824,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.g = g;
     c1.B = (int)B;
     c1.nblk = (int)nblk_conv1(g, B);
+    c1.rows = c1_rows();
     conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
     ABD_LAUNCH_CHECK();
     bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef,
@@ -1794,17 +1836,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_CONV1_BWD, s);
     ABD_LAUNCH_CHECK();
     // part rows: j*64 + c, j = 0..3 weights (kh,kw), 4 bias -> conv1.w is (c,1,kh,kw): transpose via tiny pass
-    partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, w.slab);
+    partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, nullptr, G[P_C1W], G[P_C1B]);
     ABD_LAUNCH_CHECK();
   }
   return 0;
-}
-
-__global__ void conv1_grad_scatter_kernel(const float* sums, float* gw, float* gb) {
-  const int c = threadIdx.x;
-  if (c >= 64) return;
-  for (int j = 0; j < 4; ++j) gw[c * 4 + j] = sums[j * 64 + c];
-  gb[c] = sums[4 * 64 + c];
 }
 
 DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask) {
@@ -1896,17 +1931,11 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
       P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
   ABD_LAUNCH_CHECK();
   DropArgs d1 = make_drop(a, 1, w.mask1), d2 = make_drop(a, 2, w.mask2);
-  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s)) return -1;
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked)) return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
   if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, a->metrics, s)) return -1;
   if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
-  conv1_grad_scatter_kernel<<<1, 64, 0, s>>>(w.slab, a->grads + net->off[P_C1W], a->grads + net->off[P_C1B]);
-  ABD_LAUNCH_CHECK();
   copy_masks(a, w, g, B, s);
-  if (a->num_batches_tracked) {
-    inc_i64_kernel<<<1, 64, 0, s>>>(a->num_batches_tracked, 3);
-    ABD_LAUNCH_CHECK();
-  }
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
     if (rc) return rc;
@@ -1934,16 +1963,13 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
     d1 = make_drop(a, 1, w.mask1);
     d2 = make_drop(a, 2, w.mask2);
   }
-  if (forward(net, w, P, a->x, B, a->running, train_mode ? a->running : nullptr, train_mode != 0, d1, d2, s))
+  if (forward(net, w, P, a->x, B, a->running, train_mode ? a->running : nullptr, train_mode != 0, d1, d2, s,
+              train_mode ? a->num_batches_tracked : nullptr))
     return -1;
   if (loss_and_metrics(net, w, P, nullptr, nullptr, B, 1.0f, false, w.logp, nullptr, s)) return -1;
   (void)hipMemcpyAsync(a->logprobs_out, w.logp, (size_t)B * g.K * sizeof(float), hipMemcpyDeviceToDevice, s);
   if (train_mode) {
     copy_masks(a, w, g, B, s);
-    if (a->num_batches_tracked) {
-      inc_i64_kernel<<<1, 64, 0, s>>>(a->num_batches_tracked, 3);
-      ABD_LAUNCH_CHECK();
-    }
   }
   return ABD_OK;
 }
@@ -1965,8 +1991,6 @@ int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dl
   d1.p = kP1;
   d1.scale = 1.0f / (1.0f - kP1);
   if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
-  conv1_grad_scatter_kernel<<<1, 64, 0, s>>>(w.slab, a->grads + net->off[P_C1W], a->grads + net->off[P_C1B]);
-  ABD_LAUNCH_CHECK();
   return ABD_OK;
 }
 
