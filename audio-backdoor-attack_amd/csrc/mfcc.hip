@@ -385,6 +385,54 @@ __global__ void __launch_bounds__(kThreads) db_dct_kernel(MfccDev p, const float
   }
 }
 
+// db_dct with the DCT matrix in LDS: block = (utterance, 16 frames); thread = (frame, 4
+// consecutive coefficients); the dB tile is read with broadcasts, the matrix row as float4.
+constexpr int kTT2 = 16;
+__global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const float* __restrict__ ws_db,
+                                                              const float* __restrict__ ws_max, InjDev inj,
+                                                              float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dct = sm;                           // n_mels x n_mfcc (row-major, n_mfcc % 4 == 0)
+  float* db = sm + p.n_mels * p.n_mfcc;      // kTT2 x n_mels
+  __shared__ float red[kThreads / kWave];
+  const int64_t u = blockIdx.x;
+  const int t0 = blockIdx.y * kTT2;
+  const int nt = min(kTT2, p.T - t0);
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < p.chunks; i += kThreads) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  mx = abd::wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = mx;
+  const int nd4 = p.n_mels * p.n_mfcc / 4;
+  for (int i = threadIdx.x; i < nd4; i += kThreads)
+    reinterpret_cast<float4*>(dct)[i] = reinterpret_cast<const float4*>(p.dct)[i];
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float floor_db = (p.top_db >= 0.0f) ? mx - p.top_db : -INFINITY;
+  const float* src = ws_db + ((int64_t)u * p.T + t0) * p.n_mels;
+  for (int i = threadIdx.x; i < nt * p.n_mels; i += kThreads) db[i] = fmaxf(src[i], floor_db);
+  __syncthreads();
+  const int cg4 = p.n_mfcc / 4;
+  const int t = threadIdx.x / cg4, c0 = (threadIdx.x - t * cg4) * 4;
+  if (t >= nt) return;
+  const float* d = db + t * p.n_mels;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int m = 0; m < p.n_mels; ++m) {
+    const float x = d[m];
+    const float4 w = *reinterpret_cast<const float4*>(dct + m * p.n_mfcc + c0);
+    acc.x = fmaf(x, w.x, acc.x);
+    acc.y = fmaf(x, w.y, acc.y);
+    acc.z = fmaf(x, w.z, acc.z);
+    acc.w = fmaf(x, w.w, acc.w);
+  }
+  const int tt = t0 + t;
+  if (inj.patch && row_poisoned(inj, u) && tt >= inj.pt0 && tt < inj.pt1) {
+    float* a = &acc.x;
+    for (int q = 0; q < 4; ++q)
+      if (c0 + q >= inj.pc0 && c0 + q < inj.pc1) a[q] = inj.pval;
+  }
+  *reinterpret_cast<float4*>(out + ((int64_t)u * p.T + tt) * p.n_mfcc + c0) = acc;
+}
+
 __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __restrict__ wave, int64_t row_stride,
                                                                int64_t L, const int32_t* __restrict__ rows,
                                                                InjDev inj, const float* __restrict__ rowscale,
@@ -1349,8 +1397,16 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   abd::prof_end(abd::PH_STFT_MEL, s);
   ABD_LAUNCH_CHECK();
   abd::prof_begin(abd::PH_DB_DCT, s);
-  db_dct_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT - 1) / kTT)), dim3(kThreads), 0, s>>>(d, ws_db, ws_max,
-                                                                                                   ij, out);
+  const size_t dct_lds = ((size_t)d.n_mels * d.n_mfcc + (size_t)kTT2 * d.n_mels) * sizeof(float);
+  if (d.n_mfcc % 4 == 0 && kTT2 * (d.n_mfcc / 4) <= kThreads && dct_lds <= 64 * 1024 &&
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+      getenv("ABD_DCT_GENERIC") == nullptr) {
+    db_dct_lds_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT2 - 1) / kTT2)), dim3(kThreads), dct_lds, s>>>(
+        d, ws_db, ws_max, ij, out);
+  } else {
+    db_dct_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT - 1) / kTT)), dim3(kThreads), 0, s>>>(d, ws_db, ws_max,
+                                                                                                     ij, out);
+  }
   abd::prof_end(abd::PH_DB_DCT, s);
   ABD_LAUNCH_CHECK();
   return ABD_OK;
