@@ -24,6 +24,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -520,36 +521,153 @@ struct TwTab {
 template <int N>
 __device__ constexpr TwTab<N> kTw{};
 
+// ---- butterflies on ext_vector_type(2) complex values.  Every multiplication by -i / +i is
+// written as fma(swap(d), {1,-1}, t) (exact: *1 and *-1 are exact), which the backend emits as
+// one v_pk_fma_f32 with op_sel/neg modifiers; the struct float2 versions above compile to
+// packed adds plus v_mov pairs that re-assemble halves (~27 % of the FFT's VALU).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v vswap(f2v a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ f2v fmav(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+constexpr f2v kPM = {1.0f, -1.0f};
+// t + (-i) d  and  t + i d
+__device__ __forceinline__ f2v add_mi(f2v t, f2v d) { return fmav(vswap(d), kPM, t); }
+__device__ __forceinline__ f2v add_pi(f2v t, f2v d) { return fmav(vswap(d), -kPM, t); }
+// a * w
+__device__ __forceinline__ f2v cmulv(f2v a, f2v w) {
+  const f2v ax = __builtin_shufflevector(a, a, 0, 0), ay = __builtin_shufflevector(a, a, 1, 1);
+  return fmav(ay, __builtin_shufflevector(w, -w, 3, 0), ax * w);
+}
+
 template <int R>
-__device__ __forceinline__ void dftn(float2* v);
+__device__ __forceinline__ void dftv(f2v* v);
 template <>
-__device__ __forceinline__ void dftn<2>(float2* v) { dft<2>(v); }
+__device__ __forceinline__ void dftv<2>(f2v* v) {
+  const f2v a = v[0], b = v[1];
+  v[0] = a + b;
+  v[1] = a - b;
+}
 template <>
-__device__ __forceinline__ void dftn<3>(float2* v) { dft<3>(v); }
+__device__ __forceinline__ void dftv<4>(f2v* v) {
+  const f2v t0 = v[0] + v[2], t1 = v[0] - v[2], t2 = v[1] + v[3], d = v[1] - v[3];
+  v[0] = t0 + t2;
+  v[2] = t0 - t2;
+  v[1] = add_mi(t1, d);
+  v[3] = add_pi(t1, d);
+}
 template <>
-__device__ __forceinline__ void dftn<4>(float2* v) { dft<4>(v); }
+__device__ __forceinline__ void dftv<3>(f2v* v) {
+  const float h = 0.86602540378443864676f;  // sqrt(3)/2
+  const f2v s = v[1] + v[2];
+  const f2v t = fmav(s, f2v{-0.5f, -0.5f}, v[0]);
+  const f2v d = (v[1] - v[2]) * h;
+  v[0] = v[0] + s;
+  v[1] = add_mi(t, d);
+  v[2] = add_pi(t, d);
+}
 template <>
-__device__ __forceinline__ void dftn<5>(float2* v) { dft<5>(v); }
+__device__ __forceinline__ void dftv<5>(f2v* v) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+  const f2v b1 = v[1] + v[4], b2 = v[2] + v[3], d1 = v[1] - v[4], d2 = v[2] - v[3];
+  const f2v a0 = v[0];
+  const f2v t1 = fmav(b2, f2v{c2, c2}, fmav(b1, f2v{c1, c1}, a0));
+  const f2v t2 = fmav(b2, f2v{c1, c1}, fmav(b1, f2v{c2, c2}, a0));
+  const f2v u1 = fmav(d2, f2v{s2, s2}, d1 * s1);
+  const f2v u2 = fmav(d2, f2v{-s1, -s1}, d1 * s2);
+  v[0] = a0 + b1 + b2;
+  v[1] = add_mi(t1, u1);
+  v[4] = add_pi(t1, u1);
+  v[2] = add_mi(t2, u2);
+  v[3] = add_pi(t2, u2);
+}
+
+// t * W_N^e with compile-time e: trivial angles need no multiply
+template <int N, int E>
+__device__ __forceinline__ f2v twc(f2v t) {
+  constexpr int e = E % N;
+  if constexpr (e == 0) {
+    return t;
+  } else if constexpr (4 * e == N) {  // -i
+    return __builtin_shufflevector(t, -t, 1, 2);
+  } else if constexpr (2 * e == N) {
+    return -t;
+  } else if constexpr (4 * e == 3 * N) {  // +i
+    return __builtin_shufflevector(-t, t, 1, 2);
+  } else if constexpr (8 * e == N) {  // (1 - i)/sqrt2
+    return add_mi(t, t) * 0.70710678118654752440f;
+  } else if constexpr (8 * e == 3 * N) {  // (-1 - i)/sqrt2
+    return add_mi(-t, t) * 0.70710678118654752440f;
+  } else {
+    return cmulv(t, f2v{kTw<N>.c[e], kTw<N>.s[e]});
+  }
+}
+
+template <int N1, int N2, int N2I>
+__device__ __forceinline__ void dftv_tw_col(f2v* t) {
+#pragma unroll
+  for (int k1 = 1; k1 < N1; ++k1) {
+    // k1 runtime in the unrolled loop: dispatch through a switch the compiler folds
+    switch (k1 * N2I) {
+#define ABD_TWC(E) \
+  case E: t[k1] = twc<N1 * N2, E>(t[k1]); break;
+      ABD_TWC(1) ABD_TWC(2) ABD_TWC(3) ABD_TWC(4) ABD_TWC(5) ABD_TWC(6) ABD_TWC(7) ABD_TWC(8) ABD_TWC(9)
+      ABD_TWC(10) ABD_TWC(11) ABD_TWC(12) ABD_TWC(13) ABD_TWC(14) ABD_TWC(15) ABD_TWC(16)
+#undef ABD_TWC
+      default: break;
+    }
+  }
+}
 
 // Cooley-Tukey N = N1*N2 in registers, natural-order in and out.
 template <int N1, int N2>
-__device__ __forceinline__ void dft_comp(float2* v) {
+__device__ __forceinline__ void dftv_comp(f2v* v);
+
+template <int R>
+struct DftV {
+  static __device__ __forceinline__ void run(f2v* v) { dftv<R>(v); }
+};
+template <>
+struct DftV<8> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<2, 4>(v); }
+};
+template <>
+struct DftV<9> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<3, 3>(v); }
+};
+template <>
+struct DftV<16> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<4, 4>(v); }
+};
+template <>
+struct DftV<25> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<5, 5>(v); }
+};
+
+template <int N1, int N2, int N2I>
+__device__ __forceinline__ void dftv_col(f2v* v) {
   constexpr int N = N1 * N2;
-  float2 t[N1];
+  f2v t[N1];
 #pragma unroll
-  for (int n2 = 0; n2 < N2; ++n2) {
+  for (int n1 = 0; n1 < N1; ++n1) t[n1] = v[N2 * n1 + N2I];
+  dftv<N1>(t);
+  dftv_tw_col<N1, N2, N2I>(t);
 #pragma unroll
-    for (int n1 = 0; n1 < N1; ++n1) t[n1] = v[N2 * n1 + n2];
-    dftn<N1>(t);
+  for (int k1 = 0; k1 < N1; ++k1) v[N2 * k1 + N2I] = t[k1];
+  (void)N;
+}
+
+template <int N1, int N2, int... I>
+__device__ __forceinline__ void dftv_cols(f2v* v, std::integer_sequence<int, I...>) {
+  (dftv_col<N1, N2, I>(v), ...);
+}
+
+template <int N1, int N2>
+__device__ __forceinline__ void dftv_comp(f2v* v) {
+  constexpr int N = N1 * N2;
+  dftv_cols<N1, N2>(v, std::make_integer_sequence<int, N2>{});
 #pragma unroll
-    for (int k1 = 0; k1 < N1; ++k1) {
-      const int e = (n2 * k1) % N;
-      v[N2 * k1 + n2] = (e == 0) ? t[k1] : cmul(t[k1], make_float2(kTw<N>.c[e], kTw<N>.s[e]));
-    }
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < N1; ++k1) dftn<N2>(v + N2 * k1);
-  float2 o[N];
+  for (int k1 = 0; k1 < N1; ++k1) dftv<N2>(v + N2 * k1);
+  f2v o[N];
 #pragma unroll
   for (int k1 = 0; k1 < N1; ++k1)
 #pragma unroll
@@ -557,14 +675,6 @@ __device__ __forceinline__ void dft_comp(float2* v) {
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] = o[i];
 }
-template <>
-__device__ __forceinline__ void dftn<8>(float2* v) { dft_comp<2, 4>(v); }
-template <>
-__device__ __forceinline__ void dftn<9>(float2* v) { dft_comp<3, 3>(v); }
-template <>
-__device__ __forceinline__ void dftn<16>(float2* v) { dft_comp<4, 4>(v); }
-template <>
-__device__ __forceinline__ void dftn<25>(float2* v) { dft_comp<5, 5>(v); }
 
 // threadIdx.x behind an opaque move.  The persistent item loop would otherwise hoist every
 // thread-invariant LDS/global address of all passes out of the loop and keep them live
@@ -584,10 +694,10 @@ __device__ __forceinline__ int ltid() {
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 // w[r] = w1^r for r < R by repeated squaring / one multiply (<= 4 roundings deep).
 template <int R>
-__device__ __forceinline__ void tw_powers(float2 w1, float2* w) {
+__device__ __forceinline__ void tw_powers(f2v w1, f2v* w) {
   w[1] = w1;
 #pragma unroll
-  for (int r = 2; r < R; ++r) w[r] = (r % 2 == 0) ? cmul(w[r / 2], w[r / 2]) : cmul(w[r - 1], w1);
+  for (int r = 2; r < R; ++r) w[r] = (r % 2 == 0) ? cmulv(w[r / 2], w[r / 2]) : cmulv(w[r - 1], w1);
 }
 
 // One in-place Stockham pass over PP FFTs of length M: every thread reads its butterflies
@@ -597,43 +707,53 @@ __device__ __forceinline__ void tw_powers(float2 w1, float2* w) {
 //   TWK 2: tw = W_M^k table (k < NS, NS*R == M), factor (W_M^k)^r by tw_powers
 //   VMUL : fold Bluestein's pointwise product conj(a) * vhat into the loads
 template <int M, int R, int NS, int PP, int TWK, bool VMUL>
-__device__ __forceinline__ void spass(float2* __restrict__ buf, const float2* __restrict__ tw,
-                                      const float2* __restrict__ vhat) {
+__device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* __restrict__ tws,
+                                      const float2* __restrict__ vhats) {
   constexpr int MR = M / R;
   constexpr int NB = PP * MR;
   constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
-  float2 v[ROUNDS][R];
+  f2v* buf = reinterpret_cast<f2v*>(bufs);
+  const f2v* tw = reinterpret_cast<const f2v*>(tws);
+  const f2v* vhat = reinterpret_cast<const f2v*>(vhats);
+  f2v v[ROUNDS][R];
+  const int tid = ltid();  // one value for both phases: the guards below provably agree
 #pragma unroll
   for (int rd = 0; rd < ROUNDS; ++rd) {
-    const int g = ltid() + rd * kThreads;
-    if (ROUNDS * kThreads == NB || g < NB) {
+    // wave-uniform guard: waves wholly past NB skip; the partial wave computes clamped
+    // (duplicate) butterflies and only its store is lane-guarded -- a lane-divergent guard
+    // here makes the backend zero-fill all R registers on the skip path
+    const int g = min(tid + rd * kThreads, NB - 1);
+    if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
       const int f = g / MR;
       const int j = g - f * MR;
       const int rb = f * M + j;
       const int prb = pidx(rb);
       const int k = (NS == 1) ? 0 : j % NS;
-      float2 w[R];
+      f2v w[R];
       if constexpr (TWK == 2) tw_powers<R>(tw[k], w);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         // MR % 16 == 0: pidx(rb + r MR) = pidx(rb) + r (MR + MR/16) -> base + immediate
-        float2 a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
-        if constexpr (VMUL) a = cmul(make_float2(a.x, -a.y), vhat[j + r * MR]);
+        f2v a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
+        if constexpr (VMUL) a = cmulv(a * kPM, vhat[j + r * MR]);
         if constexpr (TWK == 1) {
-          if (r > 0) a = cmul(a, tw[k * r]);
+          if (r > 0) a = cmulv(a, tw[k * r]);
         } else if constexpr (TWK == 2) {
-          if (r > 0) a = cmul(a, w[r]);
+          if (r > 0) a = cmulv(a, w[r]);
         }
         v[rd][r] = a;
       }
-      dftn<R>(v[rd]);
+      DftV<R>::run(v[rd]);
     }
   }
   __syncthreads();
 #pragma unroll
   for (int rd = 0; rd < ROUNDS; ++rd) {
-    const int g = ltid() + rd * kThreads;
-    if (ROUNDS * kThreads == NB || g < NB) {
+    // wave-uniform guard: waves wholly past NB skip; the partial wave computes clamped
+    // (duplicate) butterflies and only its store is lane-guarded -- a lane-divergent guard
+    // here makes the backend zero-fill all R registers on the skip path
+    const int g = min(tid + rd * kThreads, NB - 1);
+    if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
       const int f = g / MR;
       const int j = g - f * MR;
       const int k = (NS == 1) ? 0 : j % NS;
