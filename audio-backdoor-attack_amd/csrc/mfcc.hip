@@ -706,7 +706,9 @@ __device__ __forceinline__ void tw_powers(f2v w1, f2v* w) {
 //   TWK 1: tw = W_{NS*R}^e table, factor W_{NS*R}^{k r} read directly (k < NS, r < R)
 //   TWK 2: tw = W_M^k table (k < NS, NS*R == M), factor (W_M^k)^r by tw_powers
 //   VMUL : fold Bluestein's pointwise product conj(a) * vhat into the loads
-template <int M, int R, int NS, int PP, int TWK, bool VMUL>
+//   ZT   : rows r >= ZT are known zero (Bluestein's zero-padded input): not loaded, and the
+//          butterfly arithmetic on them folds away (mfcc.hip builds with -fno-signed-zeros)
+template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R>
 __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* __restrict__ tws,
                                       const float2* __restrict__ vhats) {
   constexpr int MR = M / R;
@@ -733,6 +735,10 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
       if constexpr (TWK == 2) tw_powers<R>(tw[k], w);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
+        if (r >= ZT) {
+          v[rd][r] = f2v{0.0f, 0.0f};
+          continue;
+        }
         // MR % 16 == 0: pidx(rb + r MR) = pidx(rb) + r (MR + MR/16) -> base + immediate
         f2v a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
         if constexpr (VMUL) a = cmulv(a * kPM, vhat[j + r * MR]);
@@ -770,10 +776,12 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
 }
 
 // tw: [W_{R0 R1}^e, e < R0 R1] ++ [W_M^k, k < R0 R1]
-template <int M, int R0, int R1, int R2, int PP, bool VMUL>
+// NZ: the input is zero beyond its first NZ elements (per FFT)
+template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M>
 __device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const float2* vhat) {
   static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
-  spass<M, R0, 1, PP, 0, VMUL>(buf, nullptr, vhat);
+  constexpr int MR0 = M / R0;
+  spass<M, R0, 1, PP, 0, VMUL, (NZ + MR0 - 1) / MR0>(buf, nullptr, vhat);
   spass<M, R1, R0, PP, 1, false>(buf, tw, nullptr);
   if constexpr (R2 > 1) spass<M, R2, R0 * R1, PP, 2, false>(buf, tw + R0 * R1, nullptr);
 }
@@ -809,10 +817,11 @@ __device__ __forceinline__ float fsample(const float* __restrict__ x, const InjD
 // zero-padded to M.  Groups of G elements per thread: all sample / chirp loads of a group
 // are issued before the first LDS store.  INTERIOR: every frame of the item lies inside the
 // signal (no padding, both frames of every pair exist), so sample addresses are affine.
-template <int M, int NN, int PP, bool BLUE, int MODE, bool INTERIOR>
+template <int M, int NN, int PP, bool BLUE, int MODE, bool INTERIOR, int NZW = M>
 __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const float* __restrict__ x, const MfccDev& p,
                                             const InjDev& inj, int pos, float rs, int p0, int np) {
-  constexpr int TOT = PP * M;
+  static_assert(PP == 1 || NZW == M, "store pruning assumes one FFT per item");
+  constexpr int TOT = PP * NZW;  // elements n >= NZW are never read by the first pass
   constexpr int ITERS = (TOT + kThreads - 1) / kThreads;
   constexpr int G = 8;
   const int L = (int)p.L;
@@ -882,14 +891,14 @@ __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const floa
   }
 }
 
-template <int M, int NN, int PP, bool BLUE, int MODE>
+template <int M, int NN, int PP, bool BLUE, int MODE, int NZW = M>
 __device__ __forceinline__ void load_item(float2* buf, const float* x, const MfccDev& p, const InjDev& inj, int pos,
                                           float rs, int p0, int np) {
   const int first = 2 * p0 * p.hop - p.pad;
   const int last_t = 2 * (p0 + PP) - 1;
   const bool interior = np == PP && first >= 0 && last_t < p.T && last_t * p.hop - p.pad + NN <= (int)p.L;
-  if (interior) load_frames<M, NN, PP, BLUE, MODE, true>(buf, x, p, inj, pos, rs, p0, np);
-  else load_frames<M, NN, PP, BLUE, MODE, false>(buf, x, p, inj, pos, rs, p0, np);
+  if (interior) load_frames<M, NN, PP, BLUE, MODE, true, NZW>(buf, x, p, inj, pos, rs, p0, np);
+  else load_frames<M, NN, PP, BLUE, MODE, false, NZW>(buf, x, p, inj, pos, rs, p0, np);
 }
 
 // Persistent blocks walk a contiguous range of (utterance, chunk) work items; each item is
@@ -899,7 +908,7 @@ __device__ __forceinline__ void load_item(float2* buf, const float* x, const Mfc
 //   -> mel by half-filter slots (2 per filter, balanced), halves combined by a lane swap
 //   -> 10 log10 -> ws_db, per-item max -> ws_max.
 template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
-__global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
+__global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
                                                                  int64_t row_stride,
                                                                  const int32_t* __restrict__ rows, int64_t batch,
                                                                  InjDev inj, const float* __restrict__ rowscale,
@@ -907,6 +916,8 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
                                                                  float* __restrict__ ws_max,
                                                                  unsigned* __restrict__ queue) {
   constexpr int NT = 2 * R0 * R1;
+  // first FFT's first pass reads rows r < ceil(N / (M/R0)) only: the rest is never stored
+  constexpr int kNZW = (BLUE && PP == 1) ? ((NN + M / R0 - 1) / (M / R0)) * (M / R0) : M;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* tw = lds;
   float2* buf = lds + NT;
@@ -955,19 +966,19 @@ __global__ void __launch_bounds__(kThreads) stft_mel_fast_kernel(MfccDev p, cons
     const int p0 = c * PP;
     const int np = min(PP, P - p0);
     switch (pois ? inj.mode : ABD_INJECT_NONE) {
-      case ABD_INJECT_ADD: load_item<M, NN, PP, BLUE, ABD_INJECT_ADD>(buf, x, p, inj, pos, rs, p0, np); break;
+      case ABD_INJECT_ADD: load_item<M, NN, PP, BLUE, ABD_INJECT_ADD, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
       case ABD_INJECT_SNR_WINDOW:
-        load_item<M, NN, PP, BLUE, ABD_INJECT_SNR_WINDOW>(buf, x, p, inj, pos, rs, p0, np);
+        load_item<M, NN, PP, BLUE, ABD_INJECT_SNR_WINDOW, kNZW>(buf, x, p, inj, pos, rs, p0, np);
         break;
       case ABD_INJECT_HALF_MIX:
-        load_item<M, NN, PP, BLUE, ABD_INJECT_HALF_MIX>(buf, x, p, inj, pos, rs, p0, np);
+        load_item<M, NN, PP, BLUE, ABD_INJECT_HALF_MIX, kNZW>(buf, x, p, inj, pos, rs, p0, np);
         break;
-      case ABD_INJECT_DEPLOY: load_item<M, NN, PP, BLUE, ABD_INJECT_DEPLOY>(buf, x, p, inj, pos, rs, p0, np); break;
-      default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE>(buf, x, p, inj, pos, rs, p0, np); break;
+      case ABD_INJECT_DEPLOY: load_item<M, NN, PP, BLUE, ABD_INJECT_DEPLOY, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
+      default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
     }
     __syncthreads();
     if (!(p.ablate & 2)) {
-      fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+      fft_plan<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr);
       if constexpr (BLUE) fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
     }
     float lmax = -INFINITY;
