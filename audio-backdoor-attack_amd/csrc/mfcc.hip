@@ -921,10 +921,16 @@ __global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(M
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* tw = lds;
   float2* buf = lds + NT;
+#ifdef ABD_MEL_W_LDS
   float* wl = reinterpret_cast<float*>(lds + NT + PP * (M + M / 16));
+#else
+  const float* wl = p.mel2_w;  // 4-5 KB, L1-resident: keeps LDS at 6 blocks/CU
+#endif
   __shared__ float red[kThreads / kWave];
   for (int i = ltid(); i < NT; i += kThreads) tw[i] = p.ftw[i];
+#ifdef ABD_MEL_W_LDS
   for (int i = ltid(); i < p.mel2_total; i += kThreads) wl[i] = p.mel2_w[i];
+#endif
   __shared__ unsigned s_item;
   const int chunks = p.chunks;
   const unsigned n_items = (unsigned)(batch * chunks);
@@ -1068,7 +1074,10 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
                 hipStream_t s) {
   auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE>;
   static_assert(M % 16 == 0, "padded LDS layout needs M % 16 == 0");
-  const size_t lds = (size_t)(2 * R0 * R1 + PP * (M + M / 16)) * sizeof(float2) + (size_t)((d.mel2_total + 3) & ~3) * 4;
+  size_t lds = (size_t)(2 * R0 * R1 + PP * (M + M / 16)) * sizeof(float2);
+#ifdef ABD_MEL_W_LDS
+  lds += (size_t)((d.mel2_total + 3) & ~3) * 4;
+#endif
   // residency from the occupancy API (VGPRs + LDS), cached per LDS size
   static size_t cached_lds = 0;
   static int cached_blocks = 0, n_cu = 0;
