@@ -10,11 +10,11 @@ root).
 from . import _lib  # noqa: F401
 from ._lib import AbdError, load_library  # noqa: F401
 
-__all__ = ["AbdError", "load_library", "features", "models", "training", "triggers", "pipeline"]
+__all__ = ["AbdError", "load_library", "features", "models", "training", "triggers", "pipeline", "flowmur"]
 
 
 def __getattr__(name):
     import importlib
-    if name in ("features", "models", "training", "triggers", "pipeline", "parallel_dp"):
+    if name in ("features", "models", "training", "triggers", "pipeline", "parallel_dp", "flowmur"):
         return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)

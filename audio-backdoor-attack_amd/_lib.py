@@ -15,17 +15,18 @@ LIB_PATH = os.environ.get("ABD_LIB", os.path.join(HERE, "libabd.so"))
 
 ABD_MEL_HTK, ABD_MEL_SLANEY = 0, 1
 ABD_PAD_REFLECT, ABD_PAD_CONSTANT = 0, 1
-INJECT_NONE, INJECT_ADD, INJECT_SNR_WINDOW, INJECT_HALF_MIX, INJECT_DEPLOY = 0, 1, 2, 3, 4
+INJECT_NONE, INJECT_ADD, INJECT_SNR_WINDOW, INJECT_HALF_MIX, INJECT_DEPLOY, INJECT_DEPLOY_CLAMP = 0, 1, 2, 3, 4, 5
 METRICS_WORDS = 8
 
 EXPORTS = (
     "abd_last_error", "abd_version",
     "abd_mfcc_plan_create", "abd_mfcc_plan_destroy", "abd_mfcc_plan_frames", "abd_mfcc_plan_describe",
     "abd_mfcc_workspace_bytes", "abd_mfcc_f32", "abd_inject_waveform_f32", "abd_inject_workspace_bytes",
-    "abd_pydub_overlay_i16",
+    "abd_pydub_overlay_i16", "abd_mfcc_deploy_backward_workspace_bytes", "abd_mfcc_deploy_backward",
     "abd_smallcnn_create", "abd_smallcnn_destroy", "abd_smallcnn_param_count", "abd_smallcnn_param_offsets",
     "abd_smallcnn_flat_features", "abd_smallcnn_workspace_bytes", "abd_smallcnn_workspace_offset", "abd_smallcnn_train_step",
     "abd_smallcnn_apply", "abd_smallcnn_forward", "abd_smallcnn_backward", "abd_smallcnn_eval", "abd_adam_f32",
+    "abd_smallcnn_input_grad_workspace_bytes", "abd_smallcnn_input_grad",
     "abd_profile_start", "abd_profile_stop",
 )
 
@@ -85,6 +86,8 @@ def _declare(lib):
         "abd_inject_waveform_f32": (i32, [vp, i64, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
         "abd_inject_workspace_bytes": (sz, [i64]),
         "abd_pydub_overlay_i16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp]),
+        "abd_mfcc_deploy_backward_workspace_bytes": (sz, [vp, i64, i64]),
+        "abd_mfcc_deploy_backward": (i32, [vp, vp, i64, vp, i64, C.POINTER(Inject), vp, vp, i32, vp, sz, vp]),
         "abd_smallcnn_create": (i32, [i32, i32, i32, i32, C.POINTER(vp)]),
         "abd_smallcnn_destroy": (None, [vp]),
         "abd_smallcnn_param_count": (i64, [vp]),
@@ -98,6 +101,8 @@ def _declare(lib):
         "abd_smallcnn_backward": (i32, [vp, C.POINTER(TrainArgs), vp, vp, sz, vp]),
         "abd_smallcnn_eval": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "abd_adam_f32": (i32, [vp, vp, vp, vp, i64, i64, f32, f32, f32, f32, vp]),
+        "abd_smallcnn_input_grad_workspace_bytes": (sz, [vp, i64]),
+        "abd_smallcnn_input_grad": (i32, [vp, vp, i64, vp, vp, vp, f32, vp, vp, vp, vp, sz, vp]),
         "abd_profile_start": (i32, [C.c_ulonglong, i32]),
         "abd_profile_stop": (i32, [C.POINTER(C.c_double), C.POINTER(i32), i32]),
     }

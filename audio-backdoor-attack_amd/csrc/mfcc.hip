@@ -57,6 +57,10 @@ struct MfccDev {
   const int4* mel2_meta;  // per half-filter slot 2m+h: (first bin, count, weight offset, 0)
   const float* mel2_w;    // compact slot weights
   int mel2_total, mel2_hp;  // #weights, max slot count rounded up to 8
+  // backward (mel^T): the <= 2 filters that touch each bin (-1 = none) and their weights
+  const int2* bin_mel;
+  const float2* bin_w;
+  int bwd_ok;  // every bin lies in at most two filters
 };
 
 struct InjDev {
@@ -176,6 +180,19 @@ __device__ __forceinline__ bool row_poisoned(const InjDev& inj, int64_t u) {
   return inj.mode != ABD_INJECT_NONE && (inj.poison == nullptr || inj.poison[u] != 0);
 }
 
+// deploy_trigger_to_waveform (utils/flowmur_generate_trigger.py:56-59) in torch's op order
+// (s*w, + t, / (s+1): each rounded, no contraction), then clamp(-1, 1) (:92) if CLAMP.
+__device__ __forceinline__ float deploy_mix(float v, float t, bool in, float rs, bool clamp) {
+  const float sv = __fmul_rn(rs, v);
+  float r = (in ? __fadd_rn(sv, t) : sv) / (rs + 1.0f);
+  if (clamp) r = fminf(fmaxf(r, -1.0f), 1.0f);
+  return r;
+}
+
+__device__ __forceinline__ bool is_deploy(int mode) {
+  return mode == ABD_INJECT_DEPLOY || mode == ABD_INJECT_DEPLOY_CLAMP;
+}
+
 // Injected sample s (0 <= s < L) of batch position u.  rs = per-row scale from the
 // norm pre-pass (SNR: trigger gain, DEPLOY: s).
 __device__ __forceinline__ float inj_sample(const float* __restrict__ x, int64_t s, const InjDev& inj,
@@ -193,10 +210,11 @@ __device__ __forceinline__ float inj_sample(const float* __restrict__ x, int64_t
       int64_t o = s - pos;
       return (o >= 0 && o < inj.trig_len) ? (v + inj.trig[o]) / 2.0f : v / 2.0f;
     }
-    case ABD_INJECT_DEPLOY: {
+    case ABD_INJECT_DEPLOY:
+    case ABD_INJECT_DEPLOY_CLAMP: {
       int64_t o = s - pos;
-      float sv = rs * v;
-      return (o >= 0 && o < inj.trig_len) ? (sv + inj.trig[o]) / (rs + 1.0f) : sv / (rs + 1.0f);
+      const bool in = o >= 0 && o < inj.trig_len;
+      return deploy_mix(v, in ? inj.trig[o] : 0.0f, in, rs, inj.mode == ABD_INJECT_DEPLOY_CLAMP);
     }
     default:
       return v;
@@ -244,7 +262,7 @@ __global__ void __launch_bounds__(kThreads) row_scale_kernel(const float* __rest
     float r = 0.0f;
     if (inj.mode == ABD_INJECT_SNR_WINDOW) {
       r = sqrtf((wn * wn) / (tn * tn) * (float)pow(10.0, -(double)inj.snr_db / 10.0));
-    } else if (inj.mode == ABD_INJECT_DEPLOY) {
+    } else if (is_deploy(inj.mode)) {
       r = (float)pow(10.0, 30.0 / 20.0) * (tn / wn);
     }
     scale[u] = r;
@@ -795,7 +813,8 @@ __device__ __forceinline__ float fsample(const float* __restrict__ x, const InjD
     const int tl = (int)inj.trig_len;
     const float t = inj.trig[min(s, tl - 1)];
     return (s < tl) ? v + t : v;
-  } else if constexpr (MODE == ABD_INJECT_SNR_WINDOW || MODE == ABD_INJECT_HALF_MIX || MODE == ABD_INJECT_DEPLOY) {
+  } else if constexpr (MODE == ABD_INJECT_SNR_WINDOW || MODE == ABD_INJECT_HALF_MIX || MODE == ABD_INJECT_DEPLOY ||
+                       MODE == ABD_INJECT_DEPLOY_CLAMP) {
     const int tl = (int)inj.trig_len;
     const int o = s - pos;
     const bool in = o >= 0 && o < tl;
@@ -805,8 +824,7 @@ __device__ __forceinline__ float fsample(const float* __restrict__ x, const InjD
     } else if constexpr (MODE == ABD_INJECT_HALF_MIX) {
       return in ? (v + t) / 2.0f : v / 2.0f;
     } else {
-      const float sv = rs * v;
-      return in ? (sv + t) / (rs + 1.0f) : sv / (rs + 1.0f);
+      return deploy_mix(v, t, in, rs, MODE == ABD_INJECT_DEPLOY_CLAMP);
     }
   } else {
     return v;
@@ -980,6 +998,9 @@ __global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(M
         load_item<M, NN, PP, BLUE, ABD_INJECT_HALF_MIX, kNZW>(buf, x, p, inj, pos, rs, p0, np);
         break;
       case ABD_INJECT_DEPLOY: load_item<M, NN, PP, BLUE, ABD_INJECT_DEPLOY, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
+      case ABD_INJECT_DEPLOY_CLAMP:
+        load_item<M, NN, PP, BLUE, ABD_INJECT_DEPLOY_CLAMP, kNZW>(buf, x, p, inj, pos, rs, p0, np);
+        break;
       default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
     }
     __syncthreads();
@@ -1057,6 +1078,249 @@ __global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(M
   }
 }
 
+// =====================================================================================
+// Backward of the MFCC w.r.t. the trigger of a DEPLOY mix: FlowMur trigger optimisation
+// (utils/flowmur_generate_trigger.py:89-104: clamp(deploy(w, t)) -> MFCC -> frozen CNN -> CE,
+// loss.backward() to t).  After a recomputed forward (stft_mel_fast_kernel -> dB, per-item max):
+//   mfcc_db_bwd_kernel : dMFCC -> d dB (DCT^T) -> top_db clamp adjoint (torch.maximum gives a
+//       tie half the gradient; amax hands the clamped mass to the maxima, split evenly) ->
+//       d mel power (10 / (ln10 x)), in place over the dB workspace
+//   stft_bwd_kernel    : per item (PP frame pairs of one utterance): the frames' FFT again,
+//       dP_k = sum_m fb[k][m] dmel[m] (<= 2 filters per bin), Y_k = dP_k conj(X_k), and
+//       g_n = 2 Re sum_{k<=N/2} Y_k W^{kn} as ONE forward FFT of the Hermitian extension of the
+//       packed pair (H_k = Y_k, H_{N-k} = conj(Y_k), H_0 = 2 Y_0, H_{N/2} = 2 Y_{N/2}: real
+//       output, frame a in .x, frame b in .y), times the window -> per-frame sample gradients
+//   wave_bwd_kernel    : overlap-add of the frames, reflect-pad adjoint, clamp mask, mix
+//       adjoint: window part dx/(s+1) per row, SNR-scale part sum dx (w - t_in)/(s+1)^2
+//   trig_coef_kernel / trig_grad_kernel : rows summed in order, plus t |t|^-2 sum_u s_u dS_u
+//       (s_u = 10^(30/20) |t| / |w_u|)
+// =====================================================================================
+constexpr float kDbAmin = -99.999f;  // 10 log10(amin = 1e-10) = -100: clamped, no gradient
+
+__global__ void __launch_bounds__(kThreads) mfcc_db_bwd_kernel(MfccDev p, const float* __restrict__ ws_max,
+                                                               const float* __restrict__ dout, float* __restrict__ db_io) {
+  extern __shared__ __attribute__((aligned(16))) float smb[];
+  float* dct = smb;                       // n_mels x n_mfcc
+  float* g = smb + p.n_mels * p.n_mfcc;   // T x n_mels: gradient kept by the top_db clamp
+  __shared__ double redd[kThreads / kWave];
+  __shared__ int redi[kThreads / kWave];
+  __shared__ float redm[kThreads / kWave];
+  const int64_t u = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < p.n_mels * p.n_mfcc; i += kThreads) dct[i] = p.dct[i];
+  float mx = -INFINITY;
+  for (int i = tid; i < p.chunks; i += kThreads) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  mx = abd::wave_max(mx);
+  if ((tid & 63) == 0) redm[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+  const float thr = (p.top_db >= 0.0f) ? mx - p.top_db : -INFINITY;
+  const int n = p.T * p.n_mels;
+  float* db = db_io + u * (int64_t)n;
+  const float* d = dout + u * (int64_t)p.T * p.n_mfcc;
+  double clamped = 0.0;
+  int nmax = 0;
+  for (int e = tid; e < n; e += kThreads) {
+    const int t = e / p.n_mels, m = e - t * p.n_mels;
+    float acc = 0.0f;
+    for (int c = 0; c < p.n_mfcc; ++c) acc = fmaf(dct[m * p.n_mfcc + c], d[t * p.n_mfcc + c], acc);
+    const float v = db[e];
+    float keep = acc;
+    if (v < thr) {
+      clamped += (double)acc;
+      keep = 0.0f;
+    } else if (v == thr) {
+      clamped += 0.5 * (double)acc;
+      keep = 0.5f * acc;
+    }
+    nmax += (v == mx) ? 1 : 0;
+    g[e] = keep;
+  }
+  clamped = abd::wave_sum_d(clamped);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmax += __shfl_xor(nmax, o, 64);
+  if ((tid & 63) == 0) {
+    redd[tid >> 6] = clamped;
+    redi[tid >> 6] = nmax;
+  }
+  __syncthreads();
+  const double cs = redd[0] + redd[1] + redd[2] + redd[3];
+  const int nm = redi[0] + redi[1] + redi[2] + redi[3];
+  const float share = (float)(cs / (double)max(nm, 1));
+  for (int e = tid; e < n; e += kThreads) {
+    const float v = db[e];
+    const float ge = g[e] + ((v == mx) ? share : 0.0f);
+    // d/dx 10 log10(max(x, amin)) = 10 / (ln10 x) above amin; x is the mel power behind v
+    const float x = exp10f(0.1f * v);
+    db[e] = (v > kDbAmin) ? ge * (4.3429448190325182f / x) : 0.0f;
+  }
+}
+
+template <int M, int R0, int R1, int R2, int PP>
+__global__ void __launch_bounds__(kThreads) stft_bwd_kernel(MfccDev p, const float* __restrict__ wave,
+                                                            int64_t row_stride, const int32_t* __restrict__ rows,
+                                                            InjDev inj, const float* __restrict__ rowscale,
+                                                            const float* __restrict__ dmel,
+                                                            float* __restrict__ gframes) {
+  constexpr int NT = 2 * R0 * R1;
+  constexpr int N = M, NF = N / 2 + 1, MP = M + M / 16;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  float2* tw = lds;
+  float2* buf = lds + NT;
+  for (int i = ltid(); i < NT; i += kThreads) tw[i] = p.ftw[i];
+  const int64_t u = blockIdx.x / p.chunks;
+  const int c = (int)(blockIdx.x - u * p.chunks);
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = wave + row * row_stride;
+  const bool pois = row_poisoned(inj, u);
+  const int pos = inj.position ? inj.position[u] : 0;
+  const float rs = rowscale ? rowscale[u] : 0.0f;
+  const int P = (p.T + 1) / 2;
+  const int p0 = c * PP;
+  const int np = min(PP, P - p0);
+  switch (pois ? inj.mode : ABD_INJECT_NONE) {
+    case ABD_INJECT_DEPLOY: load_item<M, N, PP, false, ABD_INJECT_DEPLOY>(buf, x, p, inj, pos, rs, p0, np); break;
+    case ABD_INJECT_DEPLOY_CLAMP:
+      load_item<M, N, PP, false, ABD_INJECT_DEPLOY_CLAMP>(buf, x, p, inj, pos, rs, p0, np);
+      break;
+    default: load_item<M, N, PP, false, ABD_INJECT_NONE>(buf, x, p, inj, pos, rs, p0, np); break;
+  }
+  __syncthreads();
+  fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+  // packed spectra -> Hermitian-extended packed adjoint, in place: the thread of bin k is the
+  // only reader and writer of positions k and N-k
+  for (int idx = ltid(); idx < np * NF; idx += kThreads) {
+    const int f = idx / NF, k = idx - f * NF;
+    const int kn = (k == 0) ? 0 : N - k;
+    float2* Z = buf + f * MP;
+    const float2 P1 = Z[pidx(k)], Q = Z[pidx(kn)];
+    const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
+    const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
+    const int ta = 2 * (p0 + f);
+    const int2 mm = p.bin_mel[k];
+    const float2 ww = p.bin_w[k];
+    const float* da = dmel + ((int64_t)u * p.T + ta) * p.n_mels;
+    float dpa = 0.0f, dpb = 0.0f;
+    if (mm.x >= 0) dpa = ww.x * da[mm.x];
+    if (mm.y >= 0) dpa = fmaf(ww.y, da[mm.y], dpa);
+    if (ta + 1 < p.T) {
+      const float* dbp = da + p.n_mels;
+      if (mm.x >= 0) dpb = ww.x * dbp[mm.x];
+      if (mm.y >= 0) dpb = fmaf(ww.y, dbp[mm.y], dpb);
+    }
+    // Y = dP conj(X)
+    const float yar = dpa * ar, yai = -dpa * ai, ybr = dpb * br, ybi = -dpb * bi;
+    if (k == 0 || 2 * k == N) {
+      Z[pidx(k)] = make_float2(2.0f * yar, 2.0f * ybr);  // X_0, X_{N/2} are real
+    } else {
+      Z[pidx(k)] = make_float2(yar - ybi, yai + ybr);   // Y_a + i Y_b
+      Z[pidx(kn)] = make_float2(yar + ybi, ybr - yai);  // conj(Y_a) + i conj(Y_b)
+    }
+  }
+  __syncthreads();
+  fft_plan<M, R0, R1, R2, PP, false>(buf, tw, nullptr);
+  for (int idx = ltid(); idx < np * N; idx += kThreads) {
+    const int f = idx / N, nn = idx - f * N;
+    const float2 v = buf[f * MP + pidx(nn)];
+    const float w = p.window[nn];
+    const int ta = 2 * (p0 + f);
+    gframes[((int64_t)u * p.T + ta) * N + nn] = v.x * w;
+    if (ta + 1 < p.T) gframes[((int64_t)u * p.T + ta + 1) * N + nn] = v.y * w;
+  }
+}
+
+// one thread per signal sample: overlap-add + padding adjoint + clamp mask + mix adjoint
+__global__ void __launch_bounds__(kThreads) wave_bwd_kernel(MfccDev p, const float* __restrict__ gframes,
+                                                            const float* __restrict__ wave, int64_t row_stride,
+                                                            const int32_t* __restrict__ rows, InjDev inj,
+                                                            const float* __restrict__ rowscale,
+                                                            float* __restrict__ wgrad, double* __restrict__ spart) {
+  const int64_t u = blockIdx.y;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = wave + row * row_stride;
+  const int pos = inj.position[u];
+  const float rs = rowscale[u];
+  const int L = (int)p.L, N = p.N, hop = p.hop, pad = p.pad, T = p.T;
+  const int tl = (int)inj.trig_len;
+  const float* G = gframes + u * (int64_t)T * N;
+  const int s = blockIdx.x * kThreads + threadIdx.x;
+  double part = 0.0;
+  if (s < L) {
+    // centre-padded positions that read sample s (torch reflect padding / constant)
+    int ip[3];
+    int ni = 0;
+    ip[ni++] = s + pad;
+    if (p.pad_mode != ABD_PAD_CONSTANT) {
+      if (s >= 1 && s <= pad) ip[ni++] = pad - s;
+      if (s >= L - 1 - pad && s <= L - 2) ip[ni++] = pad + 2 * (L - 1) - s;
+    }
+    float dx = 0.0f;
+    for (int q = 0; q < ni; ++q) {
+      const int i = ip[q];
+      const int a = i - N + 1;
+      const int tlo = a > 0 ? (a + hop - 1) / hop : 0;
+      const int thi = min(T - 1, i / hop);
+      for (int t = tlo; t <= thi; ++t) dx += G[(int64_t)t * N + (i - t * hop)];
+    }
+    const float v = x[s];
+    const int o = s - pos;
+    const bool in = o >= 0 && o < tl;
+    const float tv = in ? inj.trig[o] : 0.0f;
+    // torch.clamp passes the gradient for -1 <= y <= 1 only
+    if (inj.mode == ABD_INJECT_DEPLOY_CLAMP) {
+      const float y = deploy_mix(v, tv, in, rs, false);
+      if (y < -1.0f || y > 1.0f) dx = 0.0f;
+    }
+    if (in) wgrad[u * (int64_t)tl + o] = dx / (rs + 1.0f);
+    const double sp1 = (double)rs + 1.0;
+    part = (double)dx * ((double)v - (double)tv) / (sp1 * sp1);
+  }
+  __shared__ double red[kThreads / kWave];
+  part = abd::wave_sum_d(part);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) spart[u * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// coef = sum_u s_u dS_u / |t|^2, where dS_u = d loss / d s_u (one block, fixed order)
+__global__ void __launch_bounds__(kThreads) trig_coef_kernel(const double* __restrict__ spart, int nbx, int64_t B,
+                                                             const float* __restrict__ rowscale,
+                                                             const float* __restrict__ trig, int64_t tl,
+                                                             double* __restrict__ coef) {
+  double acc = 0.0, tt = 0.0;
+  for (int64_t u = threadIdx.x; u < B; u += kThreads) {
+    double su = 0.0;
+    for (int b = 0; b < nbx; ++b) su += spart[u * nbx + b];
+    acc += (double)rowscale[u] * su;
+  }
+  for (int64_t k = threadIdx.x; k < tl; k += kThreads) tt += (double)trig[k] * (double)trig[k];
+  __shared__ double red[2][kThreads / kWave];
+  acc = abd::wave_sum_d(acc);
+  tt = abd::wave_sum_d(tt);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = acc;
+    red[1][threadIdx.x >> 6] = tt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const double t2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    coef[0] = t2 > 0.0 ? a / t2 : 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) trig_grad_kernel(const float* __restrict__ wgrad, int64_t B, int64_t tl,
+                                                             const float* __restrict__ trig,
+                                                             const double* __restrict__ coef,
+                                                             float* __restrict__ dtrig, int accumulate) {
+  const int64_t k = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (k >= tl) return;
+  float s = 0.0f;
+  for (int64_t u = 0; u < B; ++u) s += wgrad[u * tl + k];
+  const float g = s + (float)(coef[0] * (double)trig[k]);
+  dtrig[k] = accumulate ? dtrig[k] + g : g;
+}
+
 struct FastPlan {
   int M, N, bluestein, pp, r0, r1;
 };
@@ -1111,6 +1375,31 @@ int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const
   if (d.M == 400 && d.N == 400 && !d.bluestein)
     return launch_fast<400, 400, 16, 25, 1, 13, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
                                                        queue, s);
+  return -1;
+}
+
+template <int M, int R0, int R1, int R2, int PP>
+int launch_stft_bwd(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
+                    const InjDev& ij, const float* rowscale, const float* dmel, float* gframes, hipStream_t s) {
+  auto* kern = &stft_bwd_kernel<M, R0, R1, R2, PP>;
+  const size_t lds = (size_t)(2 * R0 * R1 + PP * (M + M / 16)) * sizeof(float2);
+  static bool attr = false;
+  if (!attr) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr = true;
+  }
+  kern<<<(unsigned)(batch * d.chunks), kThreads, lds, s>>>(d, wave, row_stride, rows, ij, rowscale, dmel, gframes);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
+int dispatch_stft_bwd(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
+                      const InjDev& ij, const float* rowscale, const float* dmel, float* gframes, hipStream_t s) {
+  if (d.M == 2048 && d.N == 2048 && !d.bluestein && d.ppb == 4)
+    return launch_stft_bwd<2048, 16, 16, 8, 4>(d, wave, row_stride, rows, batch, ij, rowscale, dmel, gframes, s);
+  if (d.M == 400 && d.N == 400 && !d.bluestein && d.ppb == 13)
+    return launch_stft_bwd<400, 16, 25, 1, 13>(d, wave, row_stride, rows, batch, ij, rowscale, dmel, gframes, s);
   return -1;
 }
 
@@ -1348,6 +1637,27 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     }
   }
   if (mw2.empty()) mw2.push_back(0.0f);
+  // backward (mel^T): the filters touching each bin, at most two for triangular banks
+  std::vector<int2> bmel(nf, make_int2(-1, -1));
+  std::vector<float2> bw(nf, make_float2(0.0f, 0.0f));
+  d.bwd_ok = 1;
+  for (int k = 0; k < nf; ++k) {
+    int cnt = 0;
+    for (int m = 0; m < n_mels; ++m) {
+      const double v = fb[(size_t)k * n_mels + m];
+      if (v == 0.0) continue;
+      if (cnt == 0) {
+        bmel[k].x = m;
+        bw[k].x = (float)v;
+      } else if (cnt == 1) {
+        bmel[k].y = m;
+        bw[k].y = (float)v;
+      } else {
+        d.bwd_ok = 0;
+      }
+      ++cnt;
+    }
+  }
   d.mel2_total = (int)mw2.size();
   d.mel2_hp = std::max(8, (hmax + 7) / 8 * 8);
   // fast-kernel twiddles: W_{R0 R1}^e and W_M^k, e, k < R0 R1
@@ -1393,7 +1703,13 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   sz += al(meta2.size() * sizeof(int4));
   size_t off_w2 = sz;
   sz += al(mw2.size() * sizeof(float));
+  size_t off_bm = sz;
+  sz += al(nf * sizeof(int2));
+  size_t off_bw = sz;
+  sz += al(nf * sizeof(float2));
   std::vector<char> host(sz, 0);
+  memcpy(&host[off_bm], bmel.data(), nf * sizeof(int2));
+  memcpy(&host[off_bw], bw.data(), nf * sizeof(float2));
   memcpy(&host[off_tw], tw.data(), M * sizeof(float2));
   memcpy(&host[off_ci], chirp_in.data(), N * sizeof(float2));
   memcpy(&host[off_vh], vhat.data(), M * sizeof(float2));
@@ -1434,6 +1750,8 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.ftw = reinterpret_cast<const float2*>(b + off_ftw);
   d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
   d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
+  d.bin_mel = reinterpret_cast<const int2*>(b + off_bm);
+  d.bin_w = reinterpret_cast<const float2*>(b + off_bw);
   *plan = pl;
   return ABD_OK;
 }
@@ -1519,7 +1837,7 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
                                                 al((size_t)batch * sizeof(float)));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float* rowscale = nullptr;
-  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY) {
+  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP) {
     row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
     ABD_LAUNCH_CHECK();
     rowscale = ws_scale;
@@ -1564,7 +1882,7 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float* rowscale = nullptr;
-  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY) {
+  if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP) {
     ABD_CHECK(workspace && workspace_bytes >= abd_inject_workspace_bytes(batch), ABD_E_WORKSPACE,
               "workspace too small");
     row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
@@ -1575,6 +1893,77 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
   const unsigned gx = (unsigned)std::min<int64_t>((length + kThreads - 1) / kThreads, 64);
   inject_wave_kernel<<<dim3(gx, (unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
                                                                          rowscale, out);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+static int wave_blocks(const abd_mfcc_plan* plan) { return (int)((plan->dev.L + kThreads - 1) / kThreads); }
+
+size_t abd_mfcc_deploy_backward_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch, int64_t trigger_len) {
+  if (!plan) return 0;
+  const MfccDev& d = plan->dev;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return abd_mfcc_workspace_bytes(plan, batch) + al((size_t)batch * d.T * d.N * sizeof(float)) +
+         al((size_t)batch * trigger_len * sizeof(float)) + al((size_t)batch * wave_blocks(plan) * sizeof(double)) +
+         al(sizeof(double));
+}
+
+int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride, const int32_t* rows,
+                             int64_t batch, const abd_inject* inj, const float* dmfcc, float* dtrigger, int accumulate,
+                             void* workspace, size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(batch >= 1, ABD_E_INVALID, "batch must be >= 1");
+  ABD_CHECK(plan && wave && inj && dmfcc && dtrigger, ABD_E_INVALID, "NULL argument");
+  const MfccDev& d = plan->dev;
+  ABD_CHECK(d.fast && !d.bluestein && d.bwd_ok, ABD_E_UNSUPPORTED,
+            "MFCC backward needs a specialised non-Bluestein FFT plan (n_fft 2048 or 400), got n_fft %d", d.N);
+  ABD_CHECK(row_stride >= plan->length, ABD_E_INVALID, "row_stride < length");
+  InjDev ij = make_inj(inj);
+  ABD_CHECK(ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP, ABD_E_INVALID,
+            "MFCC backward is defined for the DEPLOY / DEPLOY_CLAMP mix only (got mode %d)", ij.mode);
+  ABD_CHECK(ij.poison == nullptr && !ij.patch, ABD_E_INVALID, "MFCC backward injects every row (poison must be NULL)");
+  int rc = check_inj(ij);
+  if (rc) return rc;
+  ABD_CHECK(ij.trig_len <= d.L, ABD_E_INVALID, "trigger longer than the clip");
+  const size_t need = abd_mfcc_deploy_backward_workspace_bytes(plan, batch, ij.trig_len);
+  ABD_CHECK(workspace && workspace_bytes >= need, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes,
+            need);
+  const size_t dblds = ((size_t)d.n_mels * d.n_mfcc + (size_t)d.T * d.n_mels) * sizeof(float);
+  ABD_CHECK(dblds <= 64 * 1024, ABD_E_UNSUPPORTED, "MFCC backward: %d frames x %d mels exceed the LDS tile", d.T,
+            d.n_mels);
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* ws = static_cast<char*>(workspace);
+  size_t off = 0;
+  float* ws_db = reinterpret_cast<float*>(ws + off);
+  off += al((size_t)batch * d.T * d.n_mels * sizeof(float));
+  float* ws_max = reinterpret_cast<float*>(ws + off);
+  off += al((size_t)batch * d.chunks * sizeof(float));
+  float* ws_scale = reinterpret_cast<float*>(ws + off);
+  off += al((size_t)batch * sizeof(float));
+  unsigned* queue = reinterpret_cast<unsigned*>(ws + off);
+  off = abd_mfcc_workspace_bytes(plan, batch);
+  float* gframes = reinterpret_cast<float*>(ws + off);
+  off += al((size_t)batch * d.T * d.N * sizeof(float));
+  float* wgrad = reinterpret_cast<float*>(ws + off);
+  off += al((size_t)batch * ij.trig_len * sizeof(float));
+  double* spart = reinterpret_cast<double*>(ws + off);
+  off += al((size_t)batch * wave_blocks(plan) * sizeof(double));
+  double* coef = reinterpret_cast<double*>(ws + off);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // forward recompute: SNR scale, then dB + per-item maxima (the values the clamp adjoint needs)
+  row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
+  ABD_LAUNCH_CHECK();
+  if (dispatch_fast(d, wave, row_stride, rows, batch, ij, ws_scale, ws_db, ws_max, queue, s) != 0) return -1;
+  mfcc_db_bwd_kernel<<<dim3((unsigned)batch), dim3(kThreads), dblds, s>>>(d, ws_max, dmfcc, ws_db);
+  ABD_LAUNCH_CHECK();
+  ABD_CHECK(dispatch_stft_bwd(d, wave, row_stride, rows, batch, ij, ws_scale, ws_db, gframes, s) == 0,
+            ABD_E_UNSUPPORTED, "no backward FFT plan for n_fft %d", d.N);
+  wave_bwd_kernel<<<dim3((unsigned)wave_blocks(plan), (unsigned)batch), dim3(kThreads), 0, s>>>(
+      d, gframes, wave, row_stride, rows, ij, ws_scale, wgrad, spart);
+  ABD_LAUNCH_CHECK();
+  trig_coef_kernel<<<1, kThreads, 0, s>>>(spart, wave_blocks(plan), batch, ws_scale, ij.trig, ij.trig_len, coef);
+  ABD_LAUNCH_CHECK();
+  trig_grad_kernel<<<(unsigned)((ij.trig_len + kThreads - 1) / kThreads), kThreads, 0, s>>>(
+      wgrad, batch, ij.trig_len, ij.trig, coef, dtrigger, accumulate);
   ABD_LAUNCH_CHECK();
   return ABD_OK;
 }

@@ -407,6 +407,87 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
   cgroup_partials<5, CPT>(v, 64, a.part, a.nblk, blockIdx.x);
 }
 
+// ------------------------------------------------------------------ input gradient (eval mode)
+// FlowMur's frozen benign model (utils/flowmur_generate_trigger.py:98-103) is differentiated
+// w.r.t. its input only.  Eval BatchNorm is affine, so its backward is dz = relu'(r) * alpha * dy.
+// conv1_dz_eval_kernel: thread = (utterance, conv1 row, pool1 window, 4 channels): relu(conv1)
+// recomputed, pool1 argmax, dz1 for the window's positions (NHWC).  A trailing partial window
+// (W1 % 3 != 0) gets zero.
+__global__ void __launch_bounds__(kT) conv1_dz_eval_kernel(C1Args a, float* __restrict__ dz1) {
+  const int NWx = (a.g.W1 + 2) / 3;
+  const int total = a.B * a.g.H1 * NWx * 16;
+  const int c0 = (threadIdx.x & 15) * 4;  // fixed per thread: the grid stride is a multiple of 16
+  const C1W k = c1_weights(a, c0);
+  const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
+  const float aa[4] = {al.x, al.y, al.z, al.w}, bb[4] = {be.x, be.y, be.z, be.w};
+  for (int o = blockIdx.x * kT + threadIdx.x; o < total; o += gridDim.x * kT) {
+    int q = o >> 4;
+    const int wo = q % NWx;
+    q /= NWx;
+    const int h = q % a.g.H1, b = q / a.g.H1;
+    const float* xr = a.x + ((int64_t)b * a.g.H0 + h) * a.g.W0;
+    const int w = 3 * wo;
+    const int nw = min(3, a.g.W1 - w);
+    const bool real = wo < a.g.W1p;
+    float r[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float4 v = (j < nw) ? c1_at(xr, a.g.W0, 0, w + j, k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      r[j][0] = v.x;
+      r[j][1] = v.y;
+      r[j][2] = v.z;
+      r[j][3] = v.w;
+    }
+    const float4 dy = real ? *reinterpret_cast<const float4*>(a.dp1 + (((int64_t)b * a.g.H1 + h) * a.g.W1p + wo) * 64 + c0)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dd[4] = {dy.x, dy.y, dy.z, dy.w};
+    float dz[3][4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      float best;
+      const int jm = real ? c1_argmax(r[0][qq], r[1][qq], r[2][qq], aa[qq], bb[qq], best) : -1;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dz[j][qq] = (j == jm && r[j][qq] > 0.0f) ? aa[qq] * dd[qq] : 0.0f;
+    }
+    for (int j = 0; j < nw; ++j)
+      *reinterpret_cast<float4*>(dz1 + (((int64_t)b * a.g.H1 + h) * a.g.W1 + w + j) * 64 + c0) =
+          make_float4(dz[j][0], dz[j][1], dz[j][2], dz[j][3]);
+  }
+}
+
+// dx[b][i][j] = sum_{kh,kw} sum_c conv1.w[c][kh][kw] * dz1[b][i-kh][j-kw][c]
+__global__ void __launch_bounds__(kT) conv1_dx_kernel(const float* __restrict__ w1, const float* __restrict__ dz1,
+                                                      int B, Geo g, float* __restrict__ dx) {
+  __shared__ float4 wsh[4][16];  // [tap][channel group]: 4 channels' weights
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x >> 4, cg = threadIdx.x & 15;
+    wsh[t][cg] = make_float4(w1[(4 * cg + 0) * 4 + t], w1[(4 * cg + 1) * 4 + t], w1[(4 * cg + 2) * 4 + t],
+                             w1[(4 * cg + 3) * 4 + t]);
+  }
+  __syncthreads();
+  const int total = B * g.H0 * g.W0;
+  for (int o = blockIdx.x * kT + threadIdx.x; o < total; o += gridDim.x * kT) {
+    const int b = o / (g.H0 * g.W0), rem = o - b * g.H0 * g.W0;
+    const int i = rem / g.W0, j = rem - i * g.W0;
+    float acc = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int hi = i - (t >> 1), wj = j - (t & 1);
+      if (hi < 0 || hi >= g.H1 || wj < 0 || wj >= g.W1) continue;
+      const float4* z = reinterpret_cast<const float4*>(dz1 + (((int64_t)b * g.H1 + hi) * g.W1 + wj) * 64);
+#pragma unroll 4
+      for (int cg = 0; cg < 16; ++cg) {
+        const float4 zv = z[cg], wv = wsh[t][cg];
+        acc = fmaf(zv.x, wv.x, acc);
+        acc = fmaf(zv.y, wv.y, acc);
+        acc = fmaf(zv.z, wv.z, acc);
+        acc = fmaf(zv.w, wv.w, acc);
+      }
+    }
+    dx[o] = acc;
+  }
+}
+
 // ------------------------------------------------------------------ BN statistics
 // part layout: [(j*C + c) * nblk + blk], j = 0 sum, 1 sumsq
 // nbt (optional): BatchNorm num_batches_tracked of all three layers, incremented once
@@ -453,6 +534,13 @@ __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const
   const float invstd = 1.0f / sqrtf(rv[c] + kEps);
   const float alpha = gamma[c] * invstd;
   coef[c] = make_float4(rm[c], invstd, alpha, beta[c] - rm[c] * alpha);
+}
+
+// eval BatchNorm backward as bn_dx coefficients: dx = alpha * dy (A = B = 0; the double
+// product of two floats is exact, so the result is the correctly rounded float alpha * dy)
+__global__ void bn_eval_bcoef_kernel(const float4* coef, int C, BCoef* bcoef) {
+  const int c = threadIdx.x;
+  if (c < C) bcoef[c] = BCoef{(double)coef[c].z, 0.0, 0.0, 0.0};
 }
 
 // backward finalize: s1 = sum dy (-> dbeta), s2 = sum dy*xhat (-> dgamma); coefficients for dx
@@ -2022,6 +2110,91 @@ int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* 
   if (forward(net, w, P, x, batch, running, nullptr, false, off, off, s)) return -1;
   return loss_and_metrics(net, w, P, labels, indicators, batch, 1.0f / (float)batch, false, logprobs,
                           labels ? metrics : nullptr, s);
+}
+
+static size_t dz1_bytes(const abd_cnn* net, int64_t batch) {
+  return ((size_t)batch * net->g.H1 * net->g.W1 * 64 * sizeof(float) + 255) & ~(size_t)255;
+}
+
+size_t abd_smallcnn_input_grad_workspace_bytes(const abd_cnn* net, int64_t batch) {
+  if (!net) return 0;
+  return layout(net, batch, nullptr).bytes + dz1_bytes(net, batch);
+}
+
+int abd_smallcnn_input_grad(abd_cnn* net, const float* x, int64_t batch, const float* params, const float* running,
+                            const int64_t* labels, float loss_scale, float* logprobs, float* dx, int64_t* metrics,
+                            void* workspace, size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(net && x && params && running && labels && dx, ABD_E_INVALID, "NULL argument");
+  const int64_t B = batch;
+  ABD_CHECK(B >= 1, ABD_E_INVALID, "bad batch %lld", (long long)B);
+  ABD_CHECK(B * net->g.H1 * net->g.W1 * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
+  const Work w = layout(net, B, static_cast<char*>(workspace));
+  const size_t need = w.bytes + dz1_bytes(net, B);
+  ABD_CHECK(workspace && workspace_bytes >= need, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes,
+            need);
+  float* dz1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + w.bytes);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Geo& g = net->g;
+  Params P = params_of(net, params);
+  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
+      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  ABD_LAUNCH_CHECK();
+  DropArgs off{};
+  if (forward(net, w, P, x, B, running, nullptr, false, off, off, s)) return -1;
+  if (loss_and_metrics(net, w, P, labels, nullptr, B, loss_scale / (float)B, true, logprobs ? logprobs : w.logp,
+                       metrics, s))
+    return -1;
+  // fc2 -> ReLU (no dropout in eval) -> fc1 data gradient
+  fc2_bwd_kernel<<<grid_for(B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, 1.0f, w.da);
+  ABD_LAUNCH_CHECK();
+  {
+    NTArgs a{};
+    a.src = w.da;
+    a.Hs = a.Ws = a.Ho = a.Wo = 1;
+    a.Cs = 128;
+    a.M = (int)B;
+    a.taps = 1;
+    a.Bw = w.f1t;
+    a.ldb = 128;
+    a.N = g.flat;
+    a.out = w.dp3;
+    a.ldc = g.flat;
+    if (launch_nt<128, EPI_STORE>(a, s, -1)) return -1;
+  }
+  // pool / eval BN / ReLU backward and conv data gradients, layers 3 and 2
+  for (int layer = 3; layer >= 2; --layer) {
+    const int C = layer == 3 ? 32 : 64;
+    const int co = layer == 3 ? 128 : 64;
+    bn_eval_bcoef_kernel<<<1, 64, 0, s>>>(w.coef + co, C, w.bcoef + co);
+    ABD_LAUNCH_CHECK();
+    PoolArgs pa = pool_args(g, layer, B);
+    pa.r = layer == 3 ? w.r3 : w.r2;
+    pa.coef = w.coef + co;
+    pa.dp = layer == 3 ? w.dp3 : w.dp2;
+    pa.bcoef = w.bcoef + co;
+    pa.dz = layer == 3 ? w.dz3 : w.dz2;
+    pa.part = w.part;
+    pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * C / 4);
+    bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
+    ABD_LAUNCH_CHECK();
+    NTArgs da = layer == 3 ? conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2)
+                           : conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
+    if (launch_nt<64, EPI_STORE>(da, s, -1)) return -1;
+  }
+  // layer 1: dz1 (NHWC) then the conv1 data gradient
+  C1Args c1{};
+  c1.x = x;
+  c1.w = P.p[P_C1W];
+  c1.b = P.p[P_C1B];
+  c1.coef = w.coef;
+  c1.dp1 = w.dp1;
+  c1.g = g;
+  c1.B = (int)B;
+  conv1_dz_eval_kernel<<<grid_for(B * g.H1 * ((g.W1 + 2) / 3) * 16), kT, 0, s>>>(c1, dz1);
+  ABD_LAUNCH_CHECK();
+  conv1_dx_kernel<<<grid_for(B * g.H0 * g.W0), kT, 0, s>>>(P.p[P_C1W], dz1, (int)B, g, dx);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
 }
 
 int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t step,

@@ -1,14 +1,12 @@
-"""Drop-in for utils/flowmur_generate_trigger.py (the SNR mix runs in libabd)."""
+"""Drop-in for utils/flowmur_generate_trigger.py: SNR mix, MFCC, its backward and the trigger
+optimisation loop run in libabd (abd_amd.flowmur)."""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import _root  # noqa: F401,E402
 from abd_amd.triggers import deploy_trigger_to_waveform  # noqa: F401,E402
-
-
-def generate_trigger(benign_model, dataloader, trigger_length, path):
-    raise NotImplementedError("FlowMur trigger optimisation needs backward through MFCC (SURVEY.md §8f item 1)")
+from abd_amd.flowmur import generate_trigger  # noqa: F401,E402
 
 
 def pretrain_model(train_data, train_label, test_data, test_label, path, num_classes):

@@ -65,11 +65,13 @@ size_t abd_mfcc_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch);
  *   HALF_MIX   x/2 outside, (x+t)/2 inside [p, p+Lt)                  flowmur.py:101-106
  *   DEPLOY     s=10^(30/20)|t|/|x|: (s x + t)/(s+1) inside, s x/(s+1) outside
  *                                  utils/flowmur_generate_trigger.py:49-62
+ *   DEPLOY_CLAMP  DEPLOY then clamp(-1, 1): the trigger-optimisation input
+ *                                  utils/flowmur_generate_trigger.py:91-92
  *   patch      MFCC[t0:t1, c0:c1] = value on poisoned rows        utils/badnet_trigger.py:18-27
  * poison (uint8 per batch row) selects the rows that are injected (NULL = all);
  * position (int32 per batch row) is the window start for the windowed modes. */
 enum { ABD_INJECT_NONE = 0, ABD_INJECT_ADD = 1, ABD_INJECT_SNR_WINDOW = 2,
-       ABD_INJECT_HALF_MIX = 3, ABD_INJECT_DEPLOY = 4 };
+       ABD_INJECT_HALF_MIX = 3, ABD_INJECT_DEPLOY = 4, ABD_INJECT_DEPLOY_CLAMP = 5 };
 
 typedef struct abd_inject {
   int mode;
@@ -97,6 +99,22 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
                             float* out, void* workspace, size_t workspace_bytes,
                             abd_stream_t stream);
 size_t abd_inject_workspace_bytes(int64_t batch);
+
+/* FlowMur trigger optimisation, backward half (utils/flowmur_generate_trigger.py:89-104):
+ * given dmfcc = d loss / d MFCC (batch, 1, T, n_mfcc) of
+ *     MFCC(clamp(deploy(wave, trigger, position), -1, 1))          (inj->mode DEPLOY_CLAMP;
+ *     DEPLOY skips the clamp), write d loss / d trigger (trigger_len floats) into dtrigger
+ * (accumulate != 0 adds to it).  The gradient flows through the top_db clamp (ties split
+ * like torch.maximum / amax), the dB log, the mel projection, |STFT|^2, the framing and
+ * reflect padding, the clamp, the mix and the SNR scale s = 10^(30/20)|t|/|w|.
+ * Needs a non-Bluestein specialised FFT plan (n_fft 2048 or 400; flowmur uses 2048) and
+ * inj->poison == NULL.  workspace: abd_mfcc_deploy_backward_workspace_bytes(). */
+size_t abd_mfcc_deploy_backward_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch,
+                                                int64_t trigger_len);
+int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride,
+                             const int32_t* rows, int64_t batch, const abd_inject* inj,
+                             const float* dmfcc, float* dtrigger, int accumulate,
+                             void* workspace, size_t workspace_bytes, abd_stream_t stream);
 
 /* DABA int16 path: pydub gain + overlay (utils/daba_selection_tools.py:24-39).
  * host/trig int16 (batch rows of host_len / trig_len); gain per row in dB already
@@ -180,6 +198,18 @@ int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* 
                       const float* running, const int64_t* labels,
                       const int64_t* indicators, float* logprobs, int64_t* metrics,
                       void* workspace, size_t workspace_bytes, abd_stream_t stream);
+
+/* Frozen-model input gradient (utils/flowmur_generate_trigger.py:98-103: the benign model,
+ * saved by EarlyStoppingModel right after clean_test() and therefore in eval mode, with
+ * requires_grad off): eval forward (running BN statistics, no dropout), CrossEntropyLoss on
+ * the log-probs scaled by loss_scale (mean over the batch), backward to the input x.
+ * Writes log-probs (B,K), dx (B,1,H0,W0) and, if metrics != NULL, accumulates the loss /
+ * accuracy counters.  workspace: abd_smallcnn_input_grad_workspace_bytes(). */
+size_t abd_smallcnn_input_grad_workspace_bytes(const abd_cnn* net, int64_t batch);
+int abd_smallcnn_input_grad(abd_cnn* net, const float* x, int64_t batch, const float* params,
+                            const float* running, const int64_t* labels, float loss_scale,
+                            float* logprobs, float* dx, int64_t* metrics, void* workspace,
+                            size_t workspace_bytes, abd_stream_t stream);
 
 /* torch.optim.Adam single-tensor step over a flat buffer (weight_decay 0). */
 int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,

@@ -168,6 +168,44 @@ class SmallCNN:
         z = h @ p["fc2.weight"].T + p["fc2.bias"]
         return log_softmax(z)
 
+    def input_grad_eval(self, x, labels, force=None):
+        """Eval forward + CrossEntropyLoss on the log-probs + backward to the input (the frozen
+        benign model of utils/flowmur_generate_trigger.py:98-103).  Returns (log-probs, loss, dx).
+        ``force`` replays another implementation's ReLU / pool decisions (see forward_train)."""
+        p, b = self.p, self.buf
+        h = np.asarray(x, dtype=np.float64)
+        cache = []
+        for i in (1, 2, 3):
+            z = conv2x2(h, p[f"conv{i}.weight"], p[f"conv{i}.bias"])
+            relu = z > 0
+            fi = (force or {}).get(i)
+            if fi is not None and "relu" in fi:
+                diff = fi["relu"] != relu
+                if np.any(np.abs(z[diff]) > 2e-6 * np.sqrt(np.mean(z * z))):
+                    raise AssertionError(f"layer {i}: forced ReLU decisions far from zero")
+                relu = fi["relu"]
+            r = np.where(relu, z, 0.0)
+            alpha = p[f"bn{i}.weight"] / np.sqrt(b[f"bn{i}.running_var"] + EPS)
+            y = (r - b[f"bn{i}.running_mean"][None, :, None, None]) * alpha[None, :, None, None] + \
+                p[f"bn{i}.bias"][None, :, None, None]
+            out, arg = maxpool(y, *POOLS[i], force_arg=(fi or {}).get("arg"))
+            cache.append((h, relu, alpha, arg, y.shape))
+            h = out
+        pshape = h.shape
+        flat = h.reshape(h.shape[0], -1)
+        a = flat @ p["fc1.weight"].T + p["fc1.bias"]
+        z = np.maximum(a, 0.0) @ p["fc2.weight"].T + p["fc2.bias"]
+        out = log_softmax(z)
+        loss, dz = self.ce_loss_and_grad(out, np.asarray(labels))
+        da = (dz @ p["fc2.weight"]) * (a > 0)
+        dh = (da @ p["fc1.weight"]).reshape(pshape)
+        for i in (3, 2, 1):
+            hin, relu, alpha, arg, yshape = cache[i - 1]
+            dy = maxpool_backward(dh, arg, yshape)
+            dzc = dy * alpha[None, :, None, None] * relu
+            dh, _, _ = conv2x2_backward(hin, p[f"conv{i}.weight"], dzc, need_dx=True)
+        return out, loss, dh
+
     def forward_train(self, x, mask1, mask2, force=None):
         """mask1 (B, flat) and mask2 (B, 128) keep-masks in {0,1}.
 

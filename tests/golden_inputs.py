@@ -106,5 +106,27 @@ def train_inputs(H, W, K, B, NB):
     return x, y, ind, xc, yc, xb, yb, ib
 
 
+FLOWMUR = dict(B=4, L=16000, Lt=8000, n_batches=2, epochs=2, K=10, H=32, W=13, lf=224)
+
+
+def flowmur_inputs(seed=91):
+    """FlowMur trigger-optimisation fixture inputs: int16-quantised 1 s clips (two tones + noise),
+    all labelled 2 (flowmur_generate_trigger.py:143), window positions per (epoch, batch, row)."""
+    c = FLOWMUR
+    r = rng(seed)
+    t = np.arange(c["L"]) / 16000.0
+    n = c["B"] * c["n_batches"]
+    waves = np.empty((n, c["L"]), np.float32)
+    for i in range(n):
+        f1, f2 = r.uniform(150.0, 3500.0, 2)
+        w = 0.3 * np.sin(2 * np.pi * f1 * t + r.uniform(0, 2 * np.pi)) + 0.2 * np.sin(2 * np.pi * f2 * t) * \
+            (0.5 + 0.5 * np.sin(2 * np.pi * r.uniform(2, 8) * t)) + 0.05 * r.standard_normal(c["L"])
+        waves[i] = np.round(np.clip(w, -1, 1) * 32767) / 32768.0
+    pos = r.integers(0, c["L"] - c["Lt"] + 1, (c["epochs"], c["n_batches"], c["B"]))
+    labels = np.full(c["B"], 2, np.int64)
+    state = make_state(c["H"], c["W"], c["K"], c["lf"], seed=seed + 1, trained_bn=True)
+    return waves, pos, labels, state
+
+
 def unpack_mask(packed, n_cols):
     return np.unpackbits(packed, axis=-1)[..., :n_cols].astype(np.float64)

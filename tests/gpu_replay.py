@@ -28,9 +28,9 @@ def ws_array(eng, ws, B, name, shape, dtype=torch.float32):
     return ws[off:off + n].view(dtype).view(*shape).cpu().numpy()
 
 
-def decisions(eng, B, x, params, geo):
-    """GPU decisions for the last train-mode forward kept in eng's workspace."""
-    ws = eng.workspace(B)
+def decisions(eng, B, x, params, geo, ws=None):
+    """GPU decisions for the last forward kept in eng's workspace (or ``ws``)."""
+    ws = eng.workspace(B) if ws is None else ws
     coef = ws_array(eng, ws, B, "coef", (3, 64, 4))  # (mean, invstd, alpha, beta')
     out = {}
     # layer 1: conv1 is recomputed on the device in this exact fmaf order

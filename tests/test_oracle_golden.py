@@ -174,3 +174,24 @@ def test_flowmur_injections_preserve_outside():
     assert snr == pytest.approx(30.0, abs=1e-9)
     o2 = otr.flowmur_test_inject(w, t, 10)
     np.testing.assert_allclose(o2[10:8010], (w[10:8010] + t) / 2)
+
+
+def test_flowmur_oracle_matches_autograd_golden():
+    """oracle/flowmur.py's hand-derived adjoints vs torch float64 autograd of the reference loop
+    (tests/golden/make_flowmur_golden.py): first-batch gradient and the 2x2 Adam trajectory."""
+    import os
+    from golden_inputs import FLOWMUR, flowmur_inputs
+    from oracle import flowmur as of
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "flowmur_golden.npz")))
+    c = FLOWMUR
+    waves, pos, labels, st = flowmur_inputs()
+    m = oc.SmallCNN(st)
+    B = c["B"]
+    loss, dt, feats, out = of.trigger_grad(m, waves[:B].astype(np.float64), np.full(c["Lt"], 0.1), pos[0, 0], labels)
+    assert np.abs(feats - g["feats0"]).max() < 1e-10 * np.abs(g["feats0"]).max()
+    assert abs(loss - float(g["loss0"])) < 1e-12
+    assert np.linalg.norm(dt - g["grad0"]) < 1e-10 * np.linalg.norm(g["grad0"])
+    batches = [[(waves[b * B:(b + 1) * B].astype(np.float64), labels, pos[e, b]) for b in range(c["n_batches"])]
+               for e in range(c["epochs"])]
+    traj = of.optimise(m, batches, c["Lt"], c["epochs"])
+    assert np.abs(traj - g["traj"]).max() < 1e-10
