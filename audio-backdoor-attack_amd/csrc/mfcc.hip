@@ -1095,7 +1095,8 @@ __global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(M
 //   trig_coef_kernel / trig_grad_kernel : rows summed in order, plus t |t|^-2 sum_u s_u dS_u
 //       (s_u = 10^(30/20) |t| / |w_u|)
 // =====================================================================================
-constexpr float kDbAmin = -99.999f;  // 10 log10(amin = 1e-10) = -100: clamped, no gradient
+constexpr float kDbAmin = -99.999f;
+constexpr int kWaveSpan = 1024;  // samples per wave_bwd block  // 10 log10(amin = 1e-10) = -100: clamped, no gradient
 
 __global__ void __launch_bounds__(kThreads) mfcc_db_bwd_kernel(MfccDev p, const float* __restrict__ ws_max,
                                                                const float* __restrict__ dout, float* __restrict__ db_io) {
@@ -1229,7 +1230,8 @@ __global__ void __launch_bounds__(kThreads) stft_bwd_kernel(MfccDev p, const flo
   }
 }
 
-// one thread per signal sample: overlap-add + padding adjoint + clamp mask + mix adjoint
+// block = (kWaveSpan samples, utterance), kWaveSpan / 256 samples per thread: overlap-add +
+// padding adjoint + clamp mask + mix adjoint; the SNR-scale term is reduced per block
 __global__ void __launch_bounds__(kThreads) wave_bwd_kernel(MfccDev p, const float* __restrict__ gframes,
                                                             const float* __restrict__ wave, int64_t row_stride,
                                                             const int32_t* __restrict__ rows, InjDev inj,
@@ -1243,9 +1245,12 @@ __global__ void __launch_bounds__(kThreads) wave_bwd_kernel(MfccDev p, const flo
   const int L = (int)p.L, N = p.N, hop = p.hop, pad = p.pad, T = p.T;
   const int tl = (int)inj.trig_len;
   const float* G = gframes + u * (int64_t)T * N;
-  const int s = blockIdx.x * kThreads + threadIdx.x;
+  const double sp1 = (double)rs + 1.0;
   double part = 0.0;
-  if (s < L) {
+#pragma unroll
+  for (int j = 0; j < kWaveSpan / kThreads; ++j) {
+    const int s = blockIdx.x * kWaveSpan + j * kThreads + threadIdx.x;
+    if (s >= L) break;
     // centre-padded positions that read sample s (torch reflect padding / constant)
     int ip[3];
     int ni = 0;
@@ -1272,8 +1277,7 @@ __global__ void __launch_bounds__(kThreads) wave_bwd_kernel(MfccDev p, const flo
       if (y < -1.0f || y > 1.0f) dx = 0.0f;
     }
     if (in) wgrad[u * (int64_t)tl + o] = dx / (rs + 1.0f);
-    const double sp1 = (double)rs + 1.0;
-    part = (double)dx * ((double)v - (double)tv) / (sp1 * sp1);
+    part += (double)dx * ((double)v - (double)tv) / (sp1 * sp1);
   }
   __shared__ double red[kThreads / kWave];
   part = abd::wave_sum_d(part);
@@ -1290,6 +1294,7 @@ __global__ void __launch_bounds__(kThreads) trig_coef_kernel(const double* __res
   double acc = 0.0, tt = 0.0;
   for (int64_t u = threadIdx.x; u < B; u += kThreads) {
     double su = 0.0;
+#pragma unroll 8
     for (int b = 0; b < nbx; ++b) su += spart[u * nbx + b];
     acc += (double)rowscale[u] * su;
   }
@@ -1309,16 +1314,31 @@ __global__ void __launch_bounds__(kThreads) trig_coef_kernel(const double* __res
   }
 }
 
+// dtrigger[k] = sum_u wgrad[u][k] + coef * t[k]; block = 64 consecutive k x 4 row groups, the
+// four partial sums combined in a fixed order (deterministic)
 __global__ void __launch_bounds__(kThreads) trig_grad_kernel(const float* __restrict__ wgrad, int64_t B, int64_t tl,
                                                              const float* __restrict__ trig,
                                                              const double* __restrict__ coef,
                                                              float* __restrict__ dtrig, int accumulate) {
-  const int64_t k = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-  if (k >= tl) return;
-  float s = 0.0f;
-  for (int64_t u = 0; u < B; ++u) s += wgrad[u * tl + k];
-  const float g = s + (float)(coef[0] * (double)trig[k]);
-  dtrig[k] = accumulate ? dtrig[k] + g : g;
+  __shared__ float red[4][64];
+  const int kq = threadIdx.x & 63, ug = threadIdx.x >> 6;
+  const int64_t k = blockIdx.x * (int64_t)64 + kq;
+  float s0 = 0.0f, s1 = 0.0f;
+  if (k < tl) {
+    int64_t u = ug;
+    for (; u + 4 < B; u += 8) {
+      s0 += wgrad[u * tl + k];
+      s1 += wgrad[(u + 4) * tl + k];
+    }
+    if (u < B) s0 += wgrad[u * tl + k];
+  }
+  red[ug][kq] = s0 + s1;
+  __syncthreads();
+  if (ug == 0 && k < tl) {
+    const float s = (red[0][kq] + red[1][kq]) + (red[2][kq] + red[3][kq]);
+    const float g = s + (float)(coef[0] * (double)trig[k]);
+    dtrig[k] = accumulate ? dtrig[k] + g : g;
+  }
 }
 
 struct FastPlan {
@@ -1897,7 +1917,7 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
   return ABD_OK;
 }
 
-static int wave_blocks(const abd_mfcc_plan* plan) { return (int)((plan->dev.L + kThreads - 1) / kThreads); }
+static int wave_blocks(const abd_mfcc_plan* plan) { return (int)((plan->dev.L + kWaveSpan - 1) / kWaveSpan); }
 
 size_t abd_mfcc_deploy_backward_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch, int64_t trigger_len) {
   if (!plan) return 0;
@@ -1909,7 +1929,7 @@ size_t abd_mfcc_deploy_backward_workspace_bytes(const abd_mfcc_plan* plan, int64
 }
 
 int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride, const int32_t* rows,
-                             int64_t batch, const abd_inject* inj, const float* dmfcc, float* dtrigger, int accumulate,
+                             int64_t batch, const abd_inject* inj, const float* dmfcc, float* dtrigger, int flags,
                              void* workspace, size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(batch >= 1, ABD_E_INVALID, "batch must be >= 1");
   ABD_CHECK(plan && wave && inj && dmfcc && dtrigger, ABD_E_INVALID, "NULL argument");
@@ -1949,10 +1969,12 @@ int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64
   off += al((size_t)batch * wave_blocks(plan) * sizeof(double));
   double* coef = reinterpret_cast<double*>(ws + off);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // forward recompute: SNR scale, then dB + per-item maxima (the values the clamp adjoint needs)
-  row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
-  ABD_LAUNCH_CHECK();
-  if (dispatch_fast(d, wave, row_stride, rows, batch, ij, ws_scale, ws_db, ws_max, queue, s) != 0) return -1;
+  if (!(flags & ABD_BWD_FORWARD_IN_WORKSPACE)) {
+    // forward recompute: SNR scale, then dB + per-item maxima (the values the clamp adjoint needs)
+    row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
+    ABD_LAUNCH_CHECK();
+    if (dispatch_fast(d, wave, row_stride, rows, batch, ij, ws_scale, ws_db, ws_max, queue, s) != 0) return -1;
+  }
   mfcc_db_bwd_kernel<<<dim3((unsigned)batch), dim3(kThreads), dblds, s>>>(d, ws_max, dmfcc, ws_db);
   ABD_LAUNCH_CHECK();
   ABD_CHECK(dispatch_stft_bwd(d, wave, row_stride, rows, batch, ij, ws_scale, ws_db, gframes, s) == 0,
@@ -1962,8 +1984,8 @@ int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64
   ABD_LAUNCH_CHECK();
   trig_coef_kernel<<<1, kThreads, 0, s>>>(spart, wave_blocks(plan), batch, ws_scale, ij.trig, ij.trig_len, coef);
   ABD_LAUNCH_CHECK();
-  trig_grad_kernel<<<(unsigned)((ij.trig_len + kThreads - 1) / kThreads), kThreads, 0, s>>>(
-      wgrad, batch, ij.trig_len, ij.trig, coef, dtrigger, accumulate);
+  trig_grad_kernel<<<(unsigned)((ij.trig_len + 63) / 64), kThreads, 0, s>>>(
+      wgrad, batch, ij.trig_len, ij.trig, coef, dtrigger, flags & ABD_BWD_ACCUMULATE);
   ABD_LAUNCH_CHECK();
   return ABD_OK;
 }

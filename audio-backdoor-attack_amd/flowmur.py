@@ -28,6 +28,8 @@ from . import _lib as L
 from . import features as F
 from .models import smallcnn
 
+BWD_ACCUMULATE, BWD_FORWARD_IN_WORKSPACE = 1, 2  # include/abd.h ABD_BWD_*
+
 
 def _as_abd_smallcnn(model):
     if isinstance(model, smallcnn):
@@ -89,20 +91,24 @@ class TriggerOptimizer:
         pos = torch.as_tensor(np.asarray(positions, dtype=np.int32)).to(self.dev)
         y = torch.as_tensor(labels).to(self.dev, torch.int64).contiguous()
         inj = F.Injection(mode=L.INJECT_DEPLOY_CLAMP, trigger=self.trigger, position=pos)
-        x = F.mfcc_batch(waves, self.cfg, inject=inj, out=feats_out)
+        ic = inj.to_c()
         lib = L.lib()
+        st = L.stream_ptr(self.dev)
+        # forward MFCC in the backward's workspace: its dB values / maxima / SNR scales are reused
+        ws2 = self._buf("mfcc", lib.abd_mfcc_deploy_backward_workspace_bytes(self.plan._h, B, self.Lt))
+        x = feats_out if feats_out is not None else torch.empty((B, 1, self.T, self.cfg.n_mfcc), device=self.dev)
+        L.check(lib.abd_mfcc_f32(self.plan._h, waves.data_ptr(), waves.stride(0), None, B, C.byref(ic), x.data_ptr(),
+                                 ws2.data_ptr(), ws2.numel(), st), "abd_mfcc_f32")
         dx = torch.empty_like(x)
         lp = logprobs_out if logprobs_out is not None else torch.empty((B, self.eng.K), device=self.dev)
         ws = self._buf("cnn", lib.abd_smallcnn_input_grad_workspace_bytes(self.eng.h, B))
-        st = L.stream_ptr(self.dev)
         L.check(lib.abd_smallcnn_input_grad(self.eng.h, x.data_ptr(), B, self.eng.params.data_ptr(),
                                             self.eng.running.data_ptr(), y.data_ptr(), 1.0, lp.data_ptr(),
                                             dx.data_ptr(), self.metrics.data_ptr(), ws.data_ptr(), ws.numel(), st),
                 "abd_smallcnn_input_grad")
-        ws2 = self._buf("mfcc", lib.abd_mfcc_deploy_backward_workspace_bytes(self.plan._h, B, self.Lt))
-        ic = inj.to_c()
         L.check(lib.abd_mfcc_deploy_backward(self.plan._h, waves.data_ptr(), waves.stride(0), None, B, C.byref(ic),
-                                             dx.data_ptr(), self.grad.data_ptr(), 0, ws2.data_ptr(), ws2.numel(), st),
+                                             dx.data_ptr(), self.grad.data_ptr(), BWD_FORWARD_IN_WORKSPACE,
+                                             ws2.data_ptr(), ws2.numel(), st),
                 "abd_mfcc_deploy_backward")
         return self.grad
 

@@ -103,17 +103,21 @@ size_t abd_inject_workspace_bytes(int64_t batch);
 /* FlowMur trigger optimisation, backward half (utils/flowmur_generate_trigger.py:89-104):
  * given dmfcc = d loss / d MFCC (batch, 1, T, n_mfcc) of
  *     MFCC(clamp(deploy(wave, trigger, position), -1, 1))          (inj->mode DEPLOY_CLAMP;
- *     DEPLOY skips the clamp), write d loss / d trigger (trigger_len floats) into dtrigger
- * (accumulate != 0 adds to it).  The gradient flows through the top_db clamp (ties split
+ *     DEPLOY skips the clamp), write d loss / d trigger (trigger_len floats) into dtrigger.
+ * flags: ABD_BWD_ACCUMULATE adds to dtrigger; ABD_BWD_FORWARD_IN_WORKSPACE says the same
+ * workspace just ran abd_mfcc_f32 on these inputs (its leading abd_mfcc_workspace_bytes()
+ * hold the dB values, maxima and SNR scales), so the forward is not recomputed.
+ * The gradient flows through the top_db clamp (ties split
  * like torch.maximum / amax), the dB log, the mel projection, |STFT|^2, the framing and
  * reflect padding, the clamp, the mix and the SNR scale s = 10^(30/20)|t|/|w|.
  * Needs a non-Bluestein specialised FFT plan (n_fft 2048 or 400; flowmur uses 2048) and
  * inj->poison == NULL.  workspace: abd_mfcc_deploy_backward_workspace_bytes(). */
 size_t abd_mfcc_deploy_backward_workspace_bytes(const abd_mfcc_plan* plan, int64_t batch,
                                                 int64_t trigger_len);
+enum { ABD_BWD_ACCUMULATE = 1, ABD_BWD_FORWARD_IN_WORKSPACE = 2 };
 int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride,
                              const int32_t* rows, int64_t batch, const abd_inject* inj,
-                             const float* dmfcc, float* dtrigger, int accumulate,
+                             const float* dmfcc, float* dtrigger, int flags,
                              void* workspace, size_t workspace_bytes, abd_stream_t stream);
 
 /* DABA int16 path: pydub gain + overlay (utils/daba_selection_tools.py:24-39).
