@@ -61,6 +61,7 @@ class TrainArgs(C.Structure):
         ("mask1_in", C.c_void_p), ("mask2_in", C.c_void_p), ("seed", C.c_uint64), ("counter", C.c_uint64),
         ("mask1_out", C.c_void_p), ("mask2_out", C.c_void_p), ("logprobs_out", C.c_void_p),
         ("metrics", C.c_void_p), ("grad_scale", C.c_float), ("num_batches_tracked", C.c_void_p),
+        ("fc_grads_event", C.c_void_p),
     ]
 
 

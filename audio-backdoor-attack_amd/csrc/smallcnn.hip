@@ -1783,7 +1783,7 @@ int loss_and_metrics(abd_cnn* net, const Work& w, const Params& P, const int64_t
 }
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
-             const DropArgs& drop1, hipStream_t s) {
+             const DropArgs& drop1, hipStream_t s, void* fc_grads_event) {
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -1822,6 +1822,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_FC1_WGRAD, s);
     ABD_LAUNCH_CHECK();
     if (reduce_slabs(w, nsl, 128, g.flat, 0, G[P_F1W], s)) return -1;
+  }
+  // fc1/fc2 gradients (the tail of the flat buffer, 94 % of it) are final here: a DP caller
+  // all-reduces them on a side stream while the conv backward below keeps this one busy
+  if (fc_grads_event) {
+    ABD_HIP(hipEventRecord(static_cast<hipEvent_t>(fc_grads_event), s));
   }
   // ---- fc1 data grad (NT against fc1.weight^T) * dropout1 mask
   {
@@ -2022,7 +2027,7 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked)) return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
   if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, a->metrics, s)) return -1;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event)) return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
@@ -2078,7 +2083,7 @@ int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dl
   d1.enabled = 1;
   d1.p = kP1;
   d1.scale = 1.0f / (1.0f - kP1);
-  if (backward(net, w, P, a->grads, a->x, B, d1, s)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event)) return -1;
   return ABD_OK;
 }
 

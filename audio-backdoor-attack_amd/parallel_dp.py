@@ -28,6 +28,50 @@ def allreduce_grads(flat: torch.Tensor, group=None):
     return flat
 
 
+class OverlappedGradAllReduce:
+    """Two-bucket gradient all-reduce overlapped with the conv backward.
+
+    The flat gradient buffer is laid out conv1..bn3 then fc1/fc2; the fc tail (94 % of the
+    bytes at 101x40) is final right after the fc1 weight-grad reduction, where libabd records
+    ``event`` mid-backward (abd_train_args.fc_grads_event).  ``launch_fc`` makes a side stream
+    wait for that event and starts the fc all-reduce there, so it runs over xGMI while the
+    compute stream does the conv3/conv2/conv1 backward; ``finish`` all-reduces the small conv
+    head on the compute stream and joins both before Adam.  No host synchronisation: with
+    RCCL, ``Work.wait()`` only makes the current stream wait on the collective.
+    """
+
+    def __init__(self, flat: torch.Tensor, split: int, group=None):
+        self.flat, self.split, self.group = flat, int(split), group
+        self.head, self.tail = flat[:self.split], flat[self.split:]
+        self.on_device = flat.is_cuda
+        self._work = None
+        if self.on_device:
+            self.side = torch.cuda.Stream(flat.device)
+            self.event = torch.cuda.Event()
+            self.event.record()  # materialise the hipEvent handle libabd records into
+        else:
+            self.side = self.event = None
+
+    def event_ptr(self):
+        return self.event.cuda_event if self.event is not None else None
+
+    def launch_fc(self):
+        if self.on_device:
+            self.side.wait_event(self.event)
+            with torch.cuda.stream(self.side):
+                self._work = dist.all_reduce(self.tail, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            self._work = dist.all_reduce(self.tail, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def finish(self):
+        w2 = dist.all_reduce(self.head, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        w2.wait()
+        return self.flat
+
+
 def reduce_metrics(m: torch.Tensor, group=None) -> torch.Tensor:
     """Combine libabd metric words across ranks: counts summed, batch-mean loss averaged.
 

@@ -138,6 +138,10 @@ class ResidentTrainer:
         self.gen.manual_seed(seed)
         self._epoch = None
         self._pos = 0
+        self.reducer = None
+        if world > 1:
+            split = int(model._engine.offsets[12])  # fc1.weight onwards (P_F1W)
+            self.reducer = DP.OverlappedGradAllReduce(model._engine.grads, split, process_group)
 
     # -------------------------------------------------------------- epoch plumbing
     def new_epoch(self):
@@ -164,8 +168,10 @@ class ResidentTrainer:
             T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics)
         else:
             T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics, do_update=False,
-                         grad_scale=DP.grad_scale(self.B, self.B * self.world))
-            DP.allreduce_grads(self.model._engine.grads, self.pg)
+                         grad_scale=DP.grad_scale(self.B, self.B * self.world),
+                         fc_grads_event=self.reducer.event_ptr())
+            self.reducer.launch_fc()   # fc grads all-reduce overlaps the conv backward
+            self.reducer.finish()      # conv head all-reduce, join
             T.apply_adam(self.model, self.adam, self.dev)
 
     def run_epoch(self):

@@ -73,7 +73,8 @@ def _as_long(t, device):
 
 
 def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None, metrics: torch.Tensor | None,
-               mask1=None, mask2=None, masks_out=None, do_update=True, grad_scale=1.0, seed=None, logprobs_out=None):
+               mask1=None, mask2=None, masks_out=None, do_update=True, grad_scale=1.0, seed=None, logprobs_out=None,
+               fc_grads_event=None):
     """One fused device step (forward + CE + backward [+ Adam]) -- the per-batch hot path."""
     eng = model.engine(x)
     B = x.shape[0]
@@ -99,6 +100,7 @@ def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None,
     if logprobs_out is not None:
         a.logprobs_out = logprobs_out.data_ptr()
     a.grad_scale = float(grad_scale)
+    a.fc_grads_event = fc_grads_event
     ws = eng.workspace(B)
     rc = L.lib().abd_smallcnn_train_step(eng.h, C.byref(a), ws.data_ptr(), ws.numel(), L.stream_ptr(x.device))
     L.check(rc, "abd_smallcnn_train_step")

@@ -177,6 +177,11 @@ typedef struct abd_train_args {
   int64_t* metrics;          /* ABD_METRICS_WORDS accumulators (device)       */
   float grad_scale;          /* multiply loss gradient (DP: local/global)     */
   int64_t* num_batches_tracked; /* optional int64[3] (bn1..bn3), += 1          */
+  void* fc_grads_event;      /* optional hipEvent_t, recorded on the stream once
+                              * the fc1/fc2 gradients (flat tail from offset
+                              * abd_smallcnn_param_offsets()[12]) are final, so
+                              * a DP caller can start their all-reduce while the
+                              * conv backward is still running               */
 } abd_train_args;
 
 int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspace,

@@ -48,8 +48,17 @@ def _worker(rank, world, port, q):
     m[0:1] = torch.tensor([1.5 + rank], dtype=torch.float64).view(torch.int64)
     m[1:6] = torch.tensor([B, 3 + rank, 2, 1, 4])
     red = DP.reduce_metrics(m)
+    # two-bucket overlapped all-reduce == one all-reduce of the flat buffer
+    flat = torch.tensor(r.standard_normal(1000) + rank)
+    ref = flat.clone()
+    DP.allreduce_grads(ref)
+    red2 = DP.OverlappedGradAllReduce(flat, 937)
+    assert red2.event_ptr() is None
+    red2.launch_fc()
+    red2.finish()
+    berr = float(torch.abs(flat - ref).max())
     q.put((rank, torch.cat(allrows).tolist(), float(torch.abs(local - full).max()),
-           float(red[0:1].view(torch.float64)), red[1:6].tolist()))
+           float(red[0:1].view(torch.float64)), red[1:6].tolist(), berr))
     dist.destroy_process_group()
 
 
@@ -64,7 +73,8 @@ def test_world2_sharding_gradients_and_metrics():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, allrows, gerr, loss, cnt in res:
+    for rank, allrows, gerr, loss, cnt, berr in res:
+        assert berr == 0.0                                    # bucketed == single all-reduce
         assert sorted(allrows) == list(range(64))            # disjoint cover of the epoch
         assert gerr < 1e-12                                   # sum of scaled shards == global mean grad
         assert loss == 2.0                                    # (1.5 + 2.5) / 2

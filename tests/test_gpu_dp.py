@@ -1,0 +1,101 @@
+"""GPU: the data-parallel step with the fc-gradient all-reduce overlapped with the conv backward.
+
+Two ranks share the one GPU of the test box over gloo (RCCL needs one GPU per rank; the
+8-GPU node runs the same code over RCCL).  Each rank computes its shard's gradients alone,
+all-gathers them and sums (the expected result), then re-runs the same step through
+ResidentTrainer's overlapped path (abd_train_args.fc_grads_event -> side-stream all-reduce
+of the fc tail, conv head all-reduce, join) on a gradient buffer pre-filled with a sentinel,
+so a collective that started before libabd wrote the fc gradients would show up.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import torch.distributed as dist
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import abd_amd
+        from abd_amd import features as F, synth, training as T
+        from abd_amd.models import smallcnn
+        from abd_amd.pipeline import ResidentTrainer, attack_config
+        abd_amd.load_library()
+        cfg = attack_config("badnets")
+        B, K = 32, 10
+        waves, labels = synth.make_clips_torch(128, cfg.sample_rate, cfg.length, K, seed=35 + rank, device=dev)
+        torch.manual_seed(35)
+        model = smallcnn(K, cfg.linear_features).to(dev)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+        tr = ResidentTrainer(cfg, waves, labels, model, opt, B, seed=35, rank=rank, world=world)
+        eng = model._engine
+        g = torch.Generator(device="cpu")
+        g.manual_seed(7 + rank)
+        errs = []
+        for step in range(3):
+            rows = torch.arange(step * B, (step + 1) * B, dtype=torch.int32, device=dev)
+            x = F.mfcc_batch(waves, tr.mcfg, rows=rows)
+            y = labels[rows.long()].to(dev, torch.int64)
+            ind = torch.zeros(B, dtype=torch.int64, device=dev)
+            m1 = (torch.rand((B, eng.flat), generator=g) < 0.6).to(torch.uint8).to(dev)
+            m2 = (torch.rand((B, 128), generator=g) < 0.5).to(torch.uint8).to(dev)
+            scale = 1.0 / world
+            T.train_step(model, x, y, ind, tr.adam, None, m1, m2, do_update=False, grad_scale=scale, seed=1)
+            torch.cuda.synchronize()
+            local = eng.grads.clone()
+            parts = [torch.zeros_like(local) for _ in range(world)]
+            dist.all_gather(parts, local)
+            expect = torch.stack(parts).sum(0)
+            eng.grads.fill_(1e30)
+            T.train_step(model, x, y, ind, tr.adam, None, m1, m2, do_update=False, grad_scale=scale, seed=1,
+                         fc_grads_event=tr.reducer.event_ptr())
+            tr.reducer.launch_fc()
+            tr.reducer.finish()
+            T.apply_adam(model, tr.adam, dev)
+            torch.cuda.synchronize()
+            errs.append(float(((eng.grads - expect).abs() / (expect.abs() + 1e-6)).max()))
+        p = eng.params.clone()
+        parts = [torch.zeros_like(p) for _ in range(world)]
+        dist.all_gather(parts, p)
+        same = float((parts[0] - parts[1]).abs().max())
+        q.put((rank, errs, same, None))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+        raise
+
+
+def test_overlapped_allreduce_matches_gathered_sum():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=110) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    for rank, errs, same, tb in res:
+        assert tb is None, tb
+        assert max(errs) < 1e-6, errs          # overlapped buckets == sum of the shards' gradients
+        assert same == 0.0                     # identical Adam updates on every rank
