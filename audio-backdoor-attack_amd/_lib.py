@@ -48,6 +48,7 @@ class Inject(C.Structure):
         ("patch", C.c_int),
         ("patch_t0", C.c_int), ("patch_t1", C.c_int), ("patch_c0", C.c_int), ("patch_c1", C.c_int),
         ("patch_value", C.c_float),
+        ("frames", C.c_void_p), ("frame_pad", C.c_float),
     ]
 
 
@@ -87,6 +88,16 @@ def _declare(lib):
         "abd_inject_waveform_f32": (i32, [vp, i64, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
         "abd_inject_workspace_bytes": (sz, [i64]),
         "abd_pydub_overlay_i16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp]),
+        "abd_pydub_overlay_ragged_i16": (i32, [vp, i64, vp, vp, i64, i64, vp, i64, i64, vp, vp, vp]),
+        "abd_softmax_entropy": (i32, [vp, i64, i32, vp, vp, vp]),
+        "abd_resample_plan_create": (i32, [i32, i32, i32, C.c_double, C.POINTER(vp)]),
+        "abd_resample_plan_destroy": (None, [vp]),
+        "abd_resample_output_length": (i64, [vp, i64]),
+        "abd_resample_f32": (i32, [vp, vp, i64, i64, i64, vp, i64, vp]),
+        "abd_pair_cross_entropy": (i32, [vp, vp, i64, i32, vp, vp]),
+        "abd_smallcnn_forward_per_utterance_workspace_bytes": (sz, [vp, i64]),
+        "abd_smallcnn_forward_per_utterance": (i32, [vp, vp, i64, vp, C.c_uint64, C.c_uint64, vp, vp, vp, vp, sz,
+                                                     vp]),
         "abd_mfcc_deploy_backward_workspace_bytes": (sz, [vp, i64, i64]),
         "abd_mfcc_deploy_backward": (i32, [vp, vp, i64, vp, i64, C.POINTER(Inject), vp, vp, i32, vp, sz, vp]),
         "abd_smallcnn_create": (i32, [i32, i32, i32, i32, C.POINTER(vp)]),

@@ -72,7 +72,25 @@ struct InjDev {
   float snr_db;
   int patch, pt0, pt1, pc0, pc1;
   float pval;
+  const int32_t* frames;  // ragged rows: valid frames per row (NULL = all T)
+  float fpad;             // value written to frames >= frames[row]
 };
+
+// Ragged rows (utils/daba_selection_tools.py:70-76: librosa MFCC of a shorter clip, then
+// np.pad(..., constant_values=-200) to 32 frames): the clip sits zero-extended in its row,
+// which leaves frames < 1 + len/hop exactly as librosa computes them on the short clip
+// (constant centre padding), but the top_db reference max must only see those frames.
+__device__ float ragged_db_max(const float* __restrict__ row_db, int n, float* red) {
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += kThreads) m = fmaxf(m, row_db[i]);
+  m = abd::wave_max(m);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = m;
+  __syncthreads();
+  m = red[0];
+  for (int i = 1; i < kThreads / kWave; ++i) m = fmaxf(m, red[i]);
+  return m;
+}
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -385,8 +403,14 @@ __global__ void __launch_bounds__(kThreads) db_dct_kernel(MfccDev p, const float
   const int64_t u = blockIdx.x;
   const int t0 = blockIdx.y * kTT;
   const int nt = min(kTT, p.T - t0);
+  const int nv = inj.frames ? min(max(inj.frames[u], 0), p.T) : p.T;
   float mx = -INFINITY;
-  for (int i = 0; i < p.chunks; ++i) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  if (nv < p.T) {
+    __shared__ float rred[kThreads / kWave];
+    mx = ragged_db_max(ws_db + u * p.T * p.n_mels, nv * p.n_mels, rred);
+  } else {
+    for (int i = 0; i < p.chunks; ++i) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  }
   const float floor_db = (p.top_db >= 0.0f) ? mx - p.top_db : -INFINITY;
   for (int idx = threadIdx.x; idx < nt * p.n_mels; idx += kThreads)
     db[idx] = fmaxf(ws_db[((int64_t)u * p.T + t0) * p.n_mels + idx], floor_db);
@@ -400,6 +424,7 @@ __global__ void __launch_bounds__(kThreads) db_dct_kernel(MfccDev p, const float
     for (int m = 0; m < p.n_mels; ++m) acc = fmaf(d[m], p.dct[m * p.n_mfcc + c], acc);
     const int tt = t0 + t;
     if (pois && tt >= inj.pt0 && tt < inj.pt1 && c >= inj.pc0 && c < inj.pc1) acc = inj.pval;
+    if (tt >= nv) acc = inj.fpad;
     out[((int64_t)u * p.T + tt) * p.n_mfcc + c] = acc;
   }
 }
@@ -417,8 +442,13 @@ __global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const f
   const int64_t u = blockIdx.x;
   const int t0 = blockIdx.y * kTT2;
   const int nt = min(kTT2, p.T - t0);
+  const int nv = inj.frames ? min(max(inj.frames[u], 0), p.T) : p.T;
   float mx = -INFINITY;
-  for (int i = threadIdx.x; i < p.chunks; i += kThreads) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  if (nv < p.T) {
+    for (int i = threadIdx.x; i < nv * p.n_mels; i += kThreads) mx = fmaxf(mx, ws_db[u * p.T * p.n_mels + i]);
+  } else {
+    for (int i = threadIdx.x; i < p.chunks; i += kThreads) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  }
   mx = abd::wave_max(mx);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = mx;
   const int nd4 = p.n_mels * p.n_mfcc / 4;
@@ -449,6 +479,7 @@ __global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const f
     for (int q = 0; q < 4; ++q)
       if (c0 + q >= inj.pc0 && c0 + q < inj.pc1) a[q] = inj.pval;
   }
+  if (tt >= nv) acc = make_float4(inj.fpad, inj.fpad, inj.fpad, inj.fpad);
   *reinterpret_cast<float4*>(out + ((int64_t)u * p.T + tt) * p.n_mfcc + c0) = acc;
 }
 
@@ -465,28 +496,6 @@ __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __re
   for (int64_t s = blockIdx.x * (int64_t)kThreads + threadIdx.x; s < L; s += (int64_t)gridDim.x * kThreads)
     out[u * L + s] = inj_sample(x, s, inj, pois, pos, rs);
 }
-
-__global__ void __launch_bounds__(kThreads) pydub_overlay_kernel(const int16_t* __restrict__ host, int64_t host_len,
-                                                                 const int16_t* __restrict__ trig, int64_t trig_len,
-                                                                 const float* __restrict__ gain_db,
-                                                                 int16_t* __restrict__ out) {
-  const int64_t u = blockIdx.y;
-  const double factor = pow(10.0, (double)gain_db[u] / 20.0);
-  const int64_t n = host_len < trig_len ? host_len : trig_len;
-  for (int64_t s = blockIdx.x * (int64_t)kThreads + threadIdx.x; s < host_len; s += (int64_t)gridDim.x * kThreads) {
-    int v = host[u * host_len + s];
-    if (s < n) {
-      // audioop.mul: clamp to [-32768, 32767] then floor; audioop.add: saturate.
-      double g = (double)trig[u * trig_len + s] * factor;
-      if (g > 32767.0) g = 32767.0;
-      else if (g < -32767.0) g = -32768.0;
-      v += (int)floor(g);
-      v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
-    }
-    out[u * host_len + s] = (int16_t)v;
-  }
-}
-
 
 // =====================================================================================
 // Specialised STFT+mel kernel for the attack geometries (compile-time radix plans).
@@ -1820,6 +1829,8 @@ static InjDev make_inj(const abd_inject* inj) {
   r.pc0 = inj->patch_c0;
   r.pc1 = inj->patch_c1;
   r.pval = inj->patch_value;
+  r.frames = inj->frames;
+  r.fpad = inj->frame_pad;
   if (r.mode == ABD_INJECT_NONE && r.patch) r.mode = -1;  // patch-only: rows still selected by poison
   return r;
 }
@@ -1941,6 +1952,7 @@ int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64
   ABD_CHECK(ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP, ABD_E_INVALID,
             "MFCC backward is defined for the DEPLOY / DEPLOY_CLAMP mix only (got mode %d)", ij.mode);
   ABD_CHECK(ij.poison == nullptr && !ij.patch, ABD_E_INVALID, "MFCC backward injects every row (poison must be NULL)");
+  ABD_CHECK(ij.frames == nullptr, ABD_E_UNSUPPORTED, "MFCC backward does not take ragged rows");
   int rc = check_inj(ij);
   if (rc) return rc;
   ABD_CHECK(ij.trig_len <= d.L, ABD_E_INVALID, "trigger longer than the clip");
@@ -1990,15 +2002,5 @@ int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64
   return ABD_OK;
 }
 
-int abd_pydub_overlay_i16(const int16_t* host, int64_t host_len, const int16_t* trig, int64_t trig_len,
-                          const float* gain_db, int64_t batch, int16_t* out, abd_stream_t stream) {
-  ABD_CHECK(host && trig && gain_db && out, ABD_E_INVALID, "NULL argument");
-  if (batch == 0) return ABD_OK;
-  const unsigned gx = (unsigned)std::min<int64_t>((host_len + kThreads - 1) / kThreads, 64);
-  pydub_overlay_kernel<<<dim3(gx, (unsigned)batch), dim3(kThreads), 0, static_cast<hipStream_t>(stream)>>>(
-      host, host_len, trig, trig_len, gain_db, out);
-  ABD_LAUNCH_CHECK();
-  return ABD_OK;
-}
 
 }  // extern "C"

@@ -163,6 +163,7 @@ struct C1Args {
   Geo g;
   int B;
   int rows;  // conv1 rows per chunk (<= kR1)
+  int coef_bstride;  // 0: one BN1 coefficient set; 64: per utterance (coef + b*64)
 };
 
 // Stage x rows [h0, h0+kR1] of utterance b into LDS.
@@ -272,10 +273,14 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
   const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
   const C1W k = c1_weights(a, c0);
-  const float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
+  float4 al = c1_coef_col(a.coef, c0, 2), be = c1_coef_col(a.coef, c0, 3);
   const int NW = a.g.W1p;
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    if (a.coef_bstride) {  // per-utterance BatchNorm (abd_smallcnn_forward_per_utterance)
+      al = c1_coef_col(a.coef + (int64_t)b * a.coef_bstride, c0, 2);
+      be = c1_coef_col(a.coef + (int64_t)b * a.coef_bstride, c0, 3);
+    }
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
     for (int idx = pl; idx < rows * NW; idx += 16) {
@@ -527,6 +532,100 @@ __global__ void __launch_bounds__(kT) bn_finalize_kernel(const float* part, int 
   }
 }
 
+// ------------------------------------------------------------------ per-utterance BatchNorm
+// A train-mode forward at batch 1 (utils/daba_selection_tools.py:68-87 runs the untrained
+// model that way, once per clip) normalises every utterance by its own statistics.  These
+// kernels give a whole batch of such forwards at once: one block per utterance reduces
+// sum / sumsq per channel (float per thread, double across threads) into coefficients
+// coef[b * C + c] laid out like bn_finalize_kernel's (biased variance, eps 1e-5).
+__device__ __forceinline__ float4 bn_coef_from_sums(double s, double ss, double count, float gamma, float beta) {
+  const double mean = s / count;
+  double var = ss / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)kEps));
+  const float alpha = gamma * invstd;
+  const float meanf = (float)mean;
+  return make_float4(meanf, invstd, alpha, beta - meanf * alpha);
+}
+
+// relu(conv1) statistics of utterance blockIdx.x (recomputed from x like conv1_stats_kernel)
+__global__ void __launch_bounds__(kT) inst_conv1_coef_kernel(C1Args a, const float* gamma, const float* beta,
+                                                             float4* coef) {
+  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ double red[2][16][64];
+  const int b = blockIdx.x;
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
+  const C1W k = c1_weights(a, c0);
+  float v[2][4] = {};
+  for (int hb = 0; hb < nbh; ++hb) {
+    const int h0 = hb * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    for (int idx = pl; idx < rows * a.g.W1; idx += 16) {
+      const int hl = idx / a.g.W1, w = idx - hl * a.g.W1;
+      const float4 r = c1_at(xs, a.g.W0, hl, w, k);
+      const float rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[0][q] += rr[q];
+        v[1][q] = fmaf(rr[q], rr[q], v[1][q]);
+      }
+    }
+    __syncthreads();  // xs is restaged by the next row chunk
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[0][pl][c0 + q] = (double)v[0][q];
+    red[1][pl][c0 + q] = (double)v[1][q];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    double s = 0.0, ss = 0.0;
+    for (int l = 0; l < 16; ++l) {
+      s += red[0][l][c];
+      ss += red[1][l][c];
+    }
+    coef[(int64_t)b * 64 + c] = bn_coef_from_sums(s, ss, (double)a.g.H1 * a.g.W1, gamma[c], beta[c]);
+  }
+}
+
+// statistics of an NHWC relu(conv) map (HW positions x C channels, C = 32 or 64) per utterance
+__global__ void __launch_bounds__(kT) inst_coef_kernel(const float* __restrict__ r, int HW, int C,
+                                                       const float* gamma, const float* beta, float4* coef) {
+  __shared__ double red[2][1024];
+  const int b = blockIdx.x;
+  const int CG = C / 4, lanes = kT / CG;
+  const int cg = threadIdx.x % CG, lane = threadIdx.x / CG;
+  const float* src = r + (int64_t)b * HW * C + cg * 4;
+  float v[2][4] = {};
+  for (int pos = lane; pos < HW; pos += lanes) {
+    const float4 x = *reinterpret_cast<const float4*>(src + (int64_t)pos * C);
+    const float xx[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[0][q] += xx[q];
+      v[1][q] = fmaf(xx[q], xx[q], v[1][q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[0][lane * C + cg * 4 + q] = (double)v[0][q];
+    red[1][lane * C + cg * 4 + q] = (double)v[1][q];
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    double s = 0.0, ss = 0.0;
+    for (int l = 0; l < lanes; ++l) {
+      s += red[0][l * C + c];
+      ss += red[1][l * C + c];
+    }
+    coef[(int64_t)b * C + c] = bn_coef_from_sums(s, ss, (double)HW, gamma[c], beta[c]);
+  }
+}
+
 __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, int C,
                                     float4* coef) {
   const int c = threadIdx.x;
@@ -596,6 +695,7 @@ struct PoolArgs {
   const float* r;  // NHWC (B,H,W,C) relu(conv) output
   int B, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw;
   const float4* coef;
+  int coef_bstride;  // 0: shared coefficients; C: per utterance (coef + b*C)
   float* out;      // NHWC pooled, or NCHW-flat (flat_n > 0)
   int flat_n;
   DropArgs drop;
@@ -680,7 +780,7 @@ __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
     const int c0 = wi.cg * 4;
     float4 cf[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cf[q] = a.coef[c0 + q];
+    for (int q = 0; q < 4; ++q) cf[q] = a.coef[wi.b * a.coef_bstride + c0 + q];
     float4 rv[4];
     bool in[4];
     float best[4];
@@ -1646,8 +1746,11 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
-            int64_t* nbt = nullptr) {
+            int64_t* nbt = nullptr, float4* inst_coef = nullptr) {
+  // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
+  // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
+  const bool inst = inst_coef != nullptr;
   C1Args c1{};
   c1.x = x;
   c1.w = P.p[P_C1W];
@@ -1672,7 +1775,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     rvu[2] = running_upd + 288;
   }
   // ---- layer 1
-  if (train) {
+  if (inst) {
+    inst_conv1_coef_kernel<<<(unsigned)B, kT, 0, s>>>(c1, P.p[P_BN1W], P.p[P_BN1B], inst_coef);
+    c1.coef = inst_coef;
+    c1.coef_bstride = 64;
+  } else if (train) {
     abd::prof_begin(abd::PH_CONV1_STATS, s);
     conv1_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
     abd::prof_end(abd::PH_CONV1_STATS, s);
@@ -1691,9 +1798,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     a.nblk = (a.M + kBM - 1) / kBM;
-    a.part = train ? w.part : nullptr;
+    a.part = (train && !inst) ? w.part : nullptr;
     if (launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD)) return -1;
-    if (train)
+    if (inst)
+      inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
+                                                  inst_coef + B * 64);
+    else if (train)
       bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, a.nblk, 64, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1],
                                            w.coef + 64);
     else
@@ -1701,7 +1811,8 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     ABD_LAUNCH_CHECK();
     PoolArgs pa = pool_args(g, 2, B);
     pa.r = w.r2;
-    pa.coef = w.coef + 64;
+    pa.coef = inst ? inst_coef + B * 64 : w.coef + 64;
+    pa.coef_bstride = inst ? 64 : 0;
     pa.out = w.p2;
     abd::prof_begin(abd::PH_BN2_POOL, s);
     bn_pool_fwd_kernel<<<grid_for(B * pa.Ho * pa.Wo * 64 / 4), kT, 0, s>>>(pa);
@@ -1712,9 +1823,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     a.nblk = (a.M + kBM - 1) / kBM;
-    a.part = train ? w.part : nullptr;
+    a.part = (train && !inst) ? w.part : nullptr;
     if (launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD)) return -1;
-    if (train)
+    if (inst)
+      inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
+                                                  inst_coef + B * 128);
+    else if (train)
       bn_finalize_kernel<<<32, kT, 0, s>>>(w.part, a.nblk, 32, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2],
                                            w.coef + 128);
     else
@@ -1722,7 +1836,8 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     ABD_LAUNCH_CHECK();
     PoolArgs pa = pool_args(g, 3, B);
     pa.r = w.r3;
-    pa.coef = w.coef + 128;
+    pa.coef = inst ? inst_coef + B * 128 : w.coef + 128;
+    pa.coef_bstride = inst ? 32 : 0;
     pa.out = w.p3d;
     pa.drop = drop1;
     abd::prof_begin(abd::PH_BN3_POOL, s);
@@ -2115,6 +2230,42 @@ int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* 
   if (forward(net, w, P, x, batch, running, nullptr, false, off, off, s)) return -1;
   return loss_and_metrics(net, w, P, labels, indicators, batch, 1.0f / (float)batch, false, logprobs,
                           labels ? metrics : nullptr, s);
+}
+
+static size_t inst_coef_bytes(int64_t batch) { return ((size_t)batch * 160 * sizeof(float4) + 255) & ~(size_t)255; }
+
+size_t abd_smallcnn_forward_per_utterance_workspace_bytes(const abd_cnn* net, int64_t batch) {
+  if (!net) return 0;
+  return layout(net, batch, nullptr).bytes + inst_coef_bytes(batch);
+}
+
+int abd_smallcnn_forward_per_utterance(abd_cnn* net, const float* x, int64_t batch, const float* params,
+                                       uint64_t seed, uint64_t counter, const uint8_t* mask1_in,
+                                       const uint8_t* mask2_in, float* logprobs, void* workspace,
+                                       size_t workspace_bytes, abd_stream_t stream) {
+  ABD_CHECK(net && x && params && logprobs, ABD_E_INVALID, "NULL argument");
+  if (batch == 0) return ABD_OK;
+  ABD_CHECK(batch > 0 && batch * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID,
+            "bad batch %lld (int32 activation offsets)", (long long)batch);
+  const Work w = layout(net, batch, static_cast<char*>(workspace));
+  const size_t need = w.bytes + inst_coef_bytes(batch);
+  ABD_CHECK(workspace && workspace_bytes >= need, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes,
+            need);
+  float4* icoef = reinterpret_cast<float4*>(static_cast<char*>(workspace) + w.bytes);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Geo& g = net->g;
+  Params P = params_of(net, params);
+  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
+      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  ABD_LAUNCH_CHECK();
+  abd_train_args a{};
+  a.seed = seed;
+  a.counter = counter;
+  a.mask1_in = mask1_in;
+  a.mask2_in = mask2_in;
+  DropArgs d1 = make_drop(&a, 1, w.mask1), d2 = make_drop(&a, 2, w.mask2);
+  if (forward(net, w, P, x, batch, nullptr, nullptr, true, d1, d2, s, nullptr, icoef)) return -1;
+  return loss_and_metrics(net, w, P, nullptr, nullptr, batch, 1.0f, false, logprobs, nullptr, s);
 }
 
 static size_t dz1_bytes(const abd_cnn* net, int64_t batch) {

@@ -10,7 +10,7 @@ import torch
 from torch.utils.data import Dataset
 
 import _root  # noqa: F401
-from abd_amd.features import MFCC  # noqa: F401  (prepare_dataset.py:35-47)
+from abd_amd.features import MFCC, resample  # noqa: F401  (prepare_dataset.py:35-47, :60)
 from abd_amd.io import read_wav, LABEL_SETS, train_test_split_35
 
 __all__ = ["MFCC", "BDDataset", "prepare_clean_dataset", "load_clean_data"]
@@ -32,7 +32,8 @@ class BDDataset(Dataset):
 
 def prepare_clean_dataset(data_path, directory_name, labels, waveform_to_consider, n_mfcc, n_fft, hop_length,
                           sr=16000, save=True):
-    """Load wavs (int16/32768), keep clips >= sr samples, batched MFCC on the device, 80/20 split (seed 35)."""
+    """Load wavs (int16/32768), resample to sr on the device (prepare_dataset.py:60), keep clips >= sr
+    samples, batched MFCC on the device, 80/20 split (seed 35)."""
     waves, labs = [], []
     for li, label in enumerate(labels):
         d = os.path.join(data_path, label)
@@ -40,9 +41,8 @@ def prepare_clean_dataset(data_path, directory_name, labels, waveform_to_conside
             if not name.endswith(".wav"):
                 continue
             w, rate = read_wav(os.path.join(d, name))
-            if rate != sr:
-                raise NotImplementedError(f"{name}: resampling {rate}->{sr} Hz is not implemented yet "
-                                          "(SURVEY.md §8f item 4)")
+            if rate != sr:  # only ultrasonic changes rate (16 kHz -> 44.1 kHz)
+                w = resample(torch.from_numpy(w), rate, sr).numpy()
             if w.shape[0] >= waveform_to_consider:
                 waves.append(w[None, :waveform_to_consider])
                 labs.append(li)

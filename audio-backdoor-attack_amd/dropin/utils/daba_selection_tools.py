@@ -1,4 +1,5 @@
-"""Drop-in for utils/daba_selection_tools.py: librosa MFCC and the pydub int16 overlay on the device."""
+"""Drop-in for utils/daba_selection_tools.py: librosa MFCC, the pydub int16 overlay and the
+trigger / host selection (batched per-utterance forwards) on the device."""
 import os
 import sys
 
@@ -7,6 +8,9 @@ import _root  # noqa: F401,E402
 from abd_amd.features import librosa_MFCC  # noqa: F401,E402
 from abd_amd.io import read_wav_int16, write_wav_int16  # noqa: E402
 from abd_amd import triggers as _t  # noqa: E402
+from abd_amd.daba import (get_filenames, calc_ent, cross_entropy, one_sotamax_entropy,  # noqa: F401,E402
+                          Cer_sotamax_entropy, Cer_triggers_selection, Inf_cross_entropy, Inf_hosts_selection,
+                          trigger_selection_hosts_selection, gen_trigger_variants_db)
 
 
 def single_trigger_injection_db(org_wav_path, trigger_wav_path, output_path, po_db):
@@ -16,10 +20,3 @@ def single_trigger_injection_db(org_wav_path, trigger_wav_path, output_path, po_
     out = _t.single_trigger_injection_db(host, trig, po_db)
     write_wav_int16(output_path, out, sr)
     return out, output_path
-
-
-def gen_trigger_variants_db(poison_num):
-    import random
-    random.seed(35)
-    v = [0, -5, -10, -15, -20, -25, -30, -35, -40]
-    return [v[i % len(v)] for i in random.sample(range(0, poison_num), poison_num)]

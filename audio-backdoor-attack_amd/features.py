@@ -102,6 +102,8 @@ class Injection:
     position: torch.Tensor | None = None     # int32 (B,) on device (windowed modes)
     snr_db: float = 30.0
     patch: tuple | None = None               # (t0, t1, c0, c1, value): BadNets MFCC patch
+    frames: torch.Tensor | None = None       # int32 (B,) valid frames per row (ragged clips), None = all
+    frame_pad: float = -200.0                # value of the frames past a ragged row's end
 
     def to_c(self) -> L.Inject:
         s = L.Inject()
@@ -122,6 +124,10 @@ class Injection:
             s.patch = 1
             s.patch_t0, s.patch_t1, s.patch_c0, s.patch_c1 = (int(v) for v in self.patch[:4])
             s.patch_value = float(self.patch[4])
+        if self.frames is not None:
+            assert self.frames.dtype == torch.int32 and self.frames.is_cuda
+            s.frames = self.frames.data_ptr()
+            s.frame_pad = float(self.frame_pad)
         return s
 
 
@@ -196,3 +202,50 @@ def librosa_MFCC(waveform, sample_rate, n_mfcc):
     cfg = MfccConfig.librosa(sample_rate, n_mfcc, x.shape[1])
     y = mfcc_batch(x, cfg)[0, 0].transpose(0, 1)
     return y.cpu().numpy().astype(np.float64)
+
+
+class ResamplePlan:
+    """Device polyphase sinc table for one (orig, new) rate pair (libabd abd_resample_*)."""
+
+    def __init__(self, orig_freq, new_freq, lowpass_filter_width=6, rolloff=0.99):
+        h = C.c_void_p()
+        L.check(L.lib().abd_resample_plan_create(int(orig_freq), int(new_freq), int(lowpass_filter_width),
+                                                 float(rolloff), C.byref(h)), "abd_resample_plan_create")
+        self._h = h
+
+    def output_length(self, length):
+        return int(L.lib().abd_resample_output_length(self._h, int(length)))
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) and self._h.value:
+                L.lib().abd_resample_plan_destroy(self._h)
+        except Exception:
+            pass
+
+
+_RS_PLANS: dict = {}
+
+
+def resample(waveform, orig_freq, new_freq, lowpass_filter_width=6, rolloff=0.99):
+    """torchaudio.functional.resample (sinc_interp_hann) on the HIP device -- prepare_dataset.py:60.
+
+    (..., L) float -> (..., ceil(new * L / orig)) on the input's device; equal rates return the input."""
+    t = waveform if isinstance(waveform, torch.Tensor) else torch.as_tensor(np.asarray(waveform))
+    if int(orig_freq) == int(new_freq):
+        return t
+    src_dev = t.device
+    dev = t.device if t.is_cuda else _device()
+    shape = t.shape
+    x = t.to(device=dev, dtype=torch.float32).reshape(-1, shape[-1]).contiguous()
+    key = (int(orig_freq), int(new_freq), int(lowpass_filter_width), float(rolloff), dev.index)
+    plan = _RS_PLANS.get(key)
+    if plan is None:
+        with torch.cuda.device(dev):
+            plan = ResamplePlan(orig_freq, new_freq, lowpass_filter_width, rolloff)
+        _RS_PLANS[key] = plan
+    n_out = plan.output_length(x.shape[1])
+    out = torch.empty((x.shape[0], n_out), dtype=torch.float32, device=dev)
+    L.check(L.lib().abd_resample_f32(plan._h, x.data_ptr(), x.stride(0), x.shape[0], x.shape[1], out.data_ptr(),
+                                     out.stride(0), L.stream_ptr(dev)), "abd_resample_f32")
+    return out.reshape(tuple(shape[:-1]) + (n_out,)).to(src_dev)

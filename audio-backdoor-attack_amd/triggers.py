@@ -135,6 +135,11 @@ def dbfs_int16(x: np.ndarray) -> float:
     return -math.inf if r == 0 else 20.0 * math.log10(r / 32768.0)
 
 
+def db_to_float(db: float) -> float:
+    """pydub.utils.db_to_float: the linear factor AudioSegment + dB hands audioop.mul."""
+    return 10 ** (float(db) / 20)
+
+
 def single_trigger_injection_db(host_int16, trig_int16, po_db):
     """song1.overlay(song2 + (po_db - song2.dBFS)) on int16 samples, computed by libabd."""
     h = np.asarray(host_int16, dtype=np.int16)
@@ -148,7 +153,7 @@ def single_trigger_injection_db(host_int16, trig_int16, po_db):
     dev = torch.device("cuda", torch.cuda.current_device())
     hd = torch.tensor(h[None], device=dev)
     td = torch.tensor(t[None], device=dev)
-    gd = torch.tensor([gain], dtype=torch.float32, device=dev)
+    gd = torch.tensor([db_to_float(gain)], dtype=torch.float64, device=dev)
     out = torch.empty_like(hd)
     L.check(L.lib().abd_pydub_overlay_i16(hd.data_ptr(), h.size, td.data_ptr(), t.size, gd.data_ptr(), 1,
                                           out.data_ptr(), L.stream_ptr(dev)), "abd_pydub_overlay_i16")

@@ -83,6 +83,11 @@ typedef struct abd_inject {
   int patch;
   int patch_t0, patch_t1, patch_c0, patch_c1;
   float patch_value;
+  /* ragged rows (utils/daba_selection_tools.py:70-76): frames[row] = 1 + len/hop of the
+   * clip, zero-extended in its row; the top_db max sees only those frames and later
+   * frames are set to frame_pad (-200 there).  NULL = every row has all T frames. */
+  const int32_t* frames;
+  float frame_pad;
 } abd_inject;
 
 /* wave: row-major utterances (row_stride floats apart, plan length samples each) in
@@ -121,11 +126,45 @@ int abd_mfcc_deploy_backward(const abd_mfcc_plan* plan, const float* wave, int64
                              void* workspace, size_t workspace_bytes, abd_stream_t stream);
 
 /* DABA int16 path: pydub gain + overlay (utils/daba_selection_tools.py:24-39).
- * host/trig int16 (batch rows of host_len / trig_len); gain per row in dB already
- * resolved (po_db - trig.dBFS); out int16 (batch, host_len). */
+ * host/trig int16 (batch rows of host_len / trig_len); gain per row is the LINEAR factor
+ * pydub applies, db_to_float(po_db - trig.dBFS) = 10 ** (dB / 20) evaluated in double by the
+ * caller (so audioop.mul's floor sees the same product); out int16 (batch, host_len). */
 int abd_pydub_overlay_i16(const int16_t* host, int64_t host_len, const int16_t* trig,
-                          int64_t trig_len, const float* gain_db, int64_t batch,
+                          int64_t trig_len, const double* gain, int64_t batch,
                           int16_t* out, abd_stream_t stream);
+
+/* DABA selection front end (utils/daba_selection_tools.py:24-39 + the soundfile.read that
+ * follows the wav export, :70): hosts of their own lengths host_len[row] (NULL = length),
+ * row-major with host_stride; trig rows trig_stride apart (0 = one trigger for every row).
+ * Writes `length` samples per row: the overlay inside the host, 0 past its end, as int16
+ * (out_i16) and/or as float v/32768 (out_f32); either may be NULL. */
+int abd_pydub_overlay_ragged_i16(const int16_t* host, int64_t host_stride, const int32_t* host_len,
+                                 const int16_t* trig, int64_t trig_stride, int64_t trig_len,
+                                 const double* gain, int64_t batch, int64_t length,
+                                 int16_t* out_i16, float* out_f32, abd_stream_t stream);
+
+/* utils/daba_selection_tools.py:55-65,78-81  F.softmax(output) + calc_ent (log2 entropy,
+ * double accumulation) per row of log-probs; probs (n, K) optional. */
+int abd_softmax_entropy(const float* logprobs, int64_t n, int num_classes, float* probs,
+                        double* entropy, abd_stream_t stream);
+/* utils/daba_selection_tools.py:67-68  cross_entropy(a, y) per row pair (float32, nan_to_num). */
+int abd_pair_cross_entropy(const float* probs_a, const float* probs_y, int64_t n, int num_classes,
+                           float* out, abd_stream_t stream);
+
+/* ------------------------------------------------------------------ resampling
+ * Replaces prepare_dataset.py:60  torchaudio.functional.resample(waveform, orig_freq, new_freq)
+ * (sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99 by default): 16 kHz Speech
+ * Commands -> 44.1 kHz for the ultrasonic attack.  Output length ceil(new * L / orig) on the
+ * gcd-reduced rates.  Supported: <= 448 output phases and <= 176 taps after the gcd
+ * reduction (16000 -> 44100 is 441 phases x 174 taps). */
+typedef struct abd_resample_plan abd_resample_plan;
+int abd_resample_plan_create(int orig_freq, int new_freq, int lowpass_filter_width, double rolloff,
+                             abd_resample_plan** plan);
+void abd_resample_plan_destroy(abd_resample_plan* plan);
+int64_t abd_resample_output_length(const abd_resample_plan* plan, int64_t length);
+/* in: batch rows of `length` samples, in_stride apart; out: rows of output_length, out_stride apart */
+int abd_resample_f32(const abd_resample_plan* plan, const float* in, int64_t in_stride, int64_t batch,
+                     int64_t length, float* out, int64_t out_stride, abd_stream_t stream);
 
 /* ------------------------------------------------------------------ smallcnn
  * Replaces utils/models.py:17-65 smallcnn(num_classes, linear_features) forward /
@@ -200,6 +239,18 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
                          size_t workspace_bytes, abd_stream_t stream);
 int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dlogprobs,
                           void* workspace, size_t workspace_bytes, abd_stream_t stream);
+
+/* A batch of independent batch-1 train-mode forwards (utils/daba_selection_tools.py:68-87
+ * runs the freshly built, untrained model -- nn.Module defaults to train() -- on one clip at
+ * a time): BatchNorm normalises each utterance by its OWN statistics, dropout is active
+ * (masks from mask*_in or from (seed, counter)), running statistics are left untouched (the
+ * reference's selection model is discarded).  logprobs (batch, K).
+ * workspace: abd_smallcnn_forward_per_utterance_workspace_bytes(). */
+size_t abd_smallcnn_forward_per_utterance_workspace_bytes(const abd_cnn* net, int64_t batch);
+int abd_smallcnn_forward_per_utterance(abd_cnn* net, const float* x, int64_t batch, const float* params,
+                                       uint64_t seed, uint64_t counter, const uint8_t* mask1_in,
+                                       const uint8_t* mask2_in, float* logprobs, void* workspace,
+                                       size_t workspace_bytes, abd_stream_t stream);
 
 /* eval forward (model.eval()): running BN statistics, no dropout.  Writes log-probs
  * and, if labels != NULL, accumulates loss/correct/ASR counters like test(). */

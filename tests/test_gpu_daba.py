@@ -1,0 +1,200 @@
+"""GPU parity: DABA selection (per-utterance train-mode forwards, ragged overlay + librosa MFCC,
+entropy / influence scores, batched daba_poison_data) vs the reference's golden forwards and
+the float64 oracle (oracle/daba.py)."""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import abd_amd
+from abd_amd import daba as D, models as M
+from abd_amd.io import read_wav_int16, write_wav_int16
+from golden_inputs import unpack_mask, make_state, mfcc_like, rng
+from oracle import daba as od, smallcnn as oc, triggers as ot
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "daba_golden.npz")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    abd_amd.load_library()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def dg():
+    return dict(np.load(GOLD))
+
+
+def build(st, dev):
+    m = M.smallcnn(10, 896)
+    m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
+    return m.to(dev)
+
+
+def state_of(dg):
+    return {k[6:]: v for k, v in dg.items() if k.startswith("state_")}
+
+
+def test_per_utterance_forward_matches_reference_golden(dev, dg):
+    m = build(state_of(dg), dev)
+    flat = 896
+    m1 = torch.tensor(unpack_mask(dg["mask1"], flat).astype(np.uint8), device=dev)
+    m2 = torch.tensor(unpack_mask(dg["mask2"], 128).astype(np.uint8), device=dev)
+    x = torch.tensor(dg["x"], device=dev)
+    lp = D.SelectionModel(m, dev).log_probs(x, mask1=m1, mask2=m2).cpu().numpy()
+    ref = dg["logprobs"]
+    np.testing.assert_allclose(lp, ref, rtol=RTOL, atol=RTOL * np.abs(ref).max())
+    probs, ent = D.softmax_entropy(torch.tensor(lp, device=dev))
+    np.testing.assert_allclose(probs.cpu().numpy(), dg["softmax"], rtol=RTOL, atol=1e-6)
+    np.testing.assert_allclose(ent.cpu().numpy(), [od.calc_ent(p) for p in dg["softmax"]], rtol=RTOL)
+    # running statistics untouched (the reference's selection model is thrown away)
+    assert torch.equal(m.bn1.running_mean.cpu(), torch.zeros(64))
+
+
+def test_per_utterance_forward_large_batch_vs_oracle(dev):
+    st = make_state(32, 40, 10, 896, seed=99, trained_bn=False)
+    m = build(st, dev)
+    net = oc.SmallCNN(st)
+    r = rng(5)
+    B = 300
+    x = mfcc_like(r, B, 32, 40)
+    x[::7, 0, 20:, :] = -200.0
+    m1 = (r.random((B, 896)) < 0.6).astype(np.uint8)
+    m2 = (r.random((B, 128)) < 0.5).astype(np.uint8)
+    lp = D.SelectionModel(m, dev).log_probs(torch.tensor(x, device=dev), mask1=torch.tensor(m1, device=dev),
+                                            mask2=torch.tensor(m2, device=dev), chunk=128).cpu().numpy()
+    ref = od.per_utterance_forward(net, x.astype(np.float64), m1, m2)
+    # per-row relative error; a row whose fp32 max-pool / ReLU near-tie flips is allowed to be off
+    err = np.abs(lp - ref).max(axis=1) / np.abs(ref).max(axis=1)
+    assert np.mean(err < RTOL) > 0.98, np.sort(err)[-5:]
+    assert np.median(err) < 1e-5
+
+
+def test_generated_dropout_masks_are_per_row(dev, dg):
+    m = build(state_of(dg), dev)
+    x = torch.tensor(np.repeat(dg["x"][:1], 64, axis=0), device=dev)
+    lp = D.SelectionModel(m, dev).log_probs(x, seed=123).cpu().numpy()
+    assert len({tuple(np.round(r, 4)) for r in lp}) > 60          # identical clips, independent masks
+    lp2 = D.SelectionModel(m, dev).log_probs(x, seed=123)
+    assert lp2.shape == (64, 10)
+
+
+def test_ragged_overlay_bit_exact(dev, dg):
+    trig = dg["pool1"]
+    r = rng(11)
+    hosts = [np.clip(r.normal(0, 6000, n), -32768, 32767).astype(np.int16) for n in (16000, 12000, 7000, 16000)]
+    hosts[3][:50] = 32767  # saturation
+    for po_db in (-20, 0, -40, "auto", "keep"):
+        buf, lens, Lmax = D._pack_ragged(hosts, dev)
+        tdb = D.dbfs_int16(trig)
+        gains = [0.0 if po_db == "keep" else (D.dbfs_int16(h) - tdb if po_db == "auto" else po_db - tdb)
+                 for h in hosts]
+        out = D.overlay_to_float(buf, lens, torch.tensor(trig, device=dev), D.gain_factors(gains, dev),
+                                 Lmax).cpu().numpy()
+        for i, h in enumerate(hosts):
+            exp = ot.single_trigger_injection_db(h, trig, po_db).astype(np.float64) / 32768.0
+            np.testing.assert_array_equal(out[i, :len(h)], exp.astype(np.float32))
+            assert np.all(out[i, len(h):] == 0.0)
+
+
+def test_selection_inputs_ragged_vs_oracle(dev, dg):
+    r = rng(12)
+    clips = [dg["pool0"], dg["pool2"][:11000], dg["pool3"][:5000],
+             np.clip(r.normal(0, 3000, 16000), -32768, 32767).astype(np.int16)]
+    sel = D.DabaSelector(build(state_of(dg), dev), dev)
+    x = sel.clip_inputs(clips).cpu().numpy()
+    for i, c in enumerate(clips):
+        ref = od.selection_input(c)[0, 0]
+        pad = ref == -200.0
+        assert np.array_equal(x[i, 0] == -200.0, pad)
+        scale = np.abs(ref[~pad]).max()
+        assert np.abs(x[i, 0][~pad] - ref[~pad]).max() <= 1e-4 * scale
+    # poisoned inputs: overlay then the same front end
+    xp = sel.poisoned_inputs(dg["pool1"], clips[1:3], po_db=-20).cpu().numpy()
+    for i, c in enumerate(clips[1:3]):
+        ref = od.selection_input(od.poisoned_clip(c, dg["pool1"], -20))[0, 0]
+        pad = ref == -200.0
+        assert np.array_equal(xp[i, 0] == -200.0, pad)
+        assert np.abs(xp[i, 0][~pad] - ref[~pad]).max() <= 1e-4 * np.abs(ref[~pad]).max()
+
+
+def test_certainty_and_influence_vs_oracle(dev, dg):
+    st = state_of(dg)
+    sel = D.DabaSelector(build(st, dev), dev)
+    net = oc.SmallCNN(st)
+    r = rng(13)
+    pool = [dg[f"pool{j}"] for j in range(4)]
+    P = len(pool)
+    m1 = (r.random((P, 896)) < 0.6).astype(np.uint8)
+    m2 = (r.random((P, 128)) < 0.5).astype(np.uint8)
+    ent = sel.certainty(pool, mask1=torch.tensor(m1, device=dev), mask2=torch.tensor(m2, device=dev))
+    xo = np.concatenate([od.selection_input(c) for c in pool])
+    ref_ent = [od.calc_ent(p) for p in od.softmax(od.per_utterance_forward(net, xo, m1, m2))]
+    np.testing.assert_allclose(ent, ref_ent, rtol=1e-4)
+    hosts = [np.clip(r.normal(0, 4000, n), -32768, 32767).astype(np.int16) for n in (16000, 14000, 9000, 16000, 16000)]
+    n = len(hosts)
+    tm = [torch.tensor((r.random((n, 896)) < 0.6).astype(np.uint8), device=dev),
+          torch.tensor((r.random((n, 128)) < 0.5).astype(np.uint8), device=dev)]
+    pm = [torch.tensor((r.random((n, 896)) < 0.6).astype(np.uint8), device=dev),
+          torch.tensor((r.random((n, 128)) < 0.5).astype(np.uint8), device=dev)]
+    ce = sel.influence(pool[1], hosts, po_db=-20, trig_masks=tm, pois_masks=pm)
+    xt = np.repeat(od.selection_input(pool[1]), n, axis=0)
+    xp = np.concatenate([od.selection_input(od.poisoned_clip(h, pool[1], -20)) for h in hosts])
+    pa = od.softmax(od.per_utterance_forward(net, xt, tm[0].cpu().numpy(), tm[1].cpu().numpy()))
+    py = od.softmax(od.per_utterance_forward(net, xp, pm[0].cpu().numpy(), pm[1].cpu().numpy()))
+    ref_ce = [od.cross_entropy(a, y) for a, y in zip(pa, py)]
+    np.testing.assert_allclose(ce, ref_ce, rtol=1e-4)
+
+
+def test_daba_poison_data_end_to_end(dev, dg, tmp_path):
+    """daba_poison_data on a tiny synthetic SCD tree: layout, counts, selection consistency, injected bytes."""
+    import random
+    labels = ["yes", "no", "up", "down"]
+    root = tmp_path / "scd"
+    r = rng(14)
+    for lab in labels:
+        (root / lab).mkdir(parents=True)
+        for i in range(10):
+            n = 16000 if i % 3 else 12000
+            write_wav_int16(str(root / lab / f"{lab}_{i:02d}.wav"), np.clip(r.normal(0, 3000, n), -32768,
+                                                                         32767).astype(np.int16), 16000)
+    pool = tmp_path / "pool"
+    pool.mkdir()
+    for j in range(4):
+        write_wav_int16(str(pool / f"music{j}_0.wav"), dg[f"pool{j}"], 16000)
+    out = str(tmp_path / "rec")
+    args = types.SimpleNamespace(model="smallcnn", num_classes=4)
+    random.seed(35)
+    torch.manual_seed(35)
+    trig, hosts = D.daba_poison_data(args, labels, str(root), out, "up", "Cer&Inf", True, 0.1,
+                                     trigger_pool=str(pool), n_hosts=16)
+    import json
+    cer = json.load(open(out + "/dict/Cer.json"))
+    assert trig == min(cer, key=cer.get)                          # rank-1 minimum entropy
+    inf = json.load(open(out + "/dict/Inf_hosts.json"))
+    assert sorted(hosts) == sorted(sorted(inf, key=inf.get)[:len(hosts)])
+    assert len(hosts) == round(0.1 * 32)
+    poison_files = sorted(os.listdir(out + "/poison/train/up"))
+    pf = [f for f in poison_files if f.startswith("poison_")]
+    assert 0 < len(pf) <= len(hosts)
+    assert os.path.exists(out + "/trigger.wav")
+    test_p = [f for f in os.listdir(out + "/poison/test/up") if f.startswith("poison_")]
+    assert len(test_p) > 0
+    # the poisoned train files are the pydub overlays (variant dB schedule) of hosts from the clean copy
+    tclip, _ = read_wav_int16(trig)
+    clean = {}
+    for lab in labels:
+        for f in os.listdir(out + "/clean/train/" + lab):
+            clean[f] = read_wav_int16(out + "/clean/train/" + lab + "/" + f)[0]
+    variants = D.gen_trigger_variants_db(len(hosts))
+    for f in pf:
+        k = int(f[len("poison_"):-4].lstrip("yesnodwup"))
+        got, _ = read_wav_int16(out + "/poison/train/up/" + f)
+        cands = [ot.single_trigger_injection_db(c, tclip, variants[k]) for c in clean.values() if c.size == got.size]
+        assert any(np.array_equal(got, c) for c in cands)

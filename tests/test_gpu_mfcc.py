@@ -143,9 +143,10 @@ def test_pydub_overlay_kernel(dev):
     r = np.random.default_rng(3)
     host = r.integers(-32768, 32767, (4, 1000)).astype(np.int16)
     trig = r.integers(-20000, 20000, (4, 700)).astype(np.int16)
-    gains = np.array([0.0, -12.5, 6.0, 20.0], dtype=np.float32)
+    gains = [0.0, -12.5, 6.0, 20.0]
     out = torch.empty((4, 1000), dtype=torch.int16, device=dev)
-    hd, td, gd = (torch.tensor(a, device=dev) for a in (host, trig, gains))
+    hd, td = (torch.tensor(a, device=dev) for a in (host, trig))
+    gd = torch.tensor([10 ** (g / 20) for g in gains], dtype=torch.float64, device=dev)  # pydub db_to_float
     L.check(L.lib().abd_pydub_overlay_i16(hd.data_ptr(), 1000, td.data_ptr(), 700, gd.data_ptr(), 4, out.data_ptr(),
                                           L.stream_ptr()), "overlay")
     exp = np.stack([otr.pydub_overlay(host[i], otr.pydub_gain(trig[i], float(gains[i]))) for i in range(4)])
