@@ -52,6 +52,13 @@ class Inject(C.Structure):
     ]
 
 
+class Effect(C.Structure):
+    _fields_ = [("kind", C.c_int), ("p", C.c_float * 5)]
+
+
+FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER = 0, 1, 2, 3
+
+
 class TrainArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("labels", C.c_void_p), ("indicators", C.c_void_p), ("batch", C.c_int64),
@@ -90,6 +97,9 @@ def _declare(lib):
         "abd_pydub_overlay_i16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp]),
         "abd_pydub_overlay_ragged_i16": (i32, [vp, i64, vp, vp, i64, i64, vp, i64, i64, vp, vp, vp]),
         "abd_softmax_entropy": (i32, [vp, i64, i32, vp, vp, vp]),
+        "abd_style_board_create": (i32, [C.POINTER(Effect), i32, i32, i64, C.POINTER(vp)]),
+        "abd_style_board_destroy": (None, [vp]),
+        "abd_style_board_apply": (i32, [vp, vp, i64, vp, i64, i64, vp, i64, vp]),
         "abd_resample_plan_create": (i32, [i32, i32, i32, C.c_double, C.POINTER(vp)]),
         "abd_resample_plan_destroy": (None, [vp]),
         "abd_resample_output_length": (i64, [vp, i64]),

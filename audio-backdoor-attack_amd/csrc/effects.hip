@@ -1,0 +1,274 @@
+// JingleBack style boards (utils/styles_trigger.py:8-53, jingleback.py:38-119) on the device.
+//
+// pedalboard runs JUCE dsp processors in float32, one clip per call with reset=True, so every
+// clip starts from zeroed filter state and snapped parameter smoothers.  The effects the
+// default board (style 5: Gain(12) -> LadderFilter(HPF12, 1 kHz) -> Phaser()) and style 1
+// (Distortion(30)) use are restated from the JUCE algorithms:
+//   Gain          x * Decibels::decibelsToGain(dB)                       (float pow)
+//   Distortion    tanh(x * decibelsToGain(drive_db))                     (Gain -> WaveShaper)
+//   LadderFilter  juce::dsp::LadderFilter<float>::processSample: tanh saturation through a
+//                 128-point LookupTableTransform over [-5, 5], a 4-pole one-sample-delay
+//                 ladder with resonance feedback from the last pole, mode mix A[0..4]
+//   Phaser        juce::dsp::Phaser<float>: a 1 Hz sine LFO evaluated every 4th sample
+//                 (juce::dsp::Oscillator at sr/4, float phase accumulator), mapped log-wise
+//                 to a cutoff in [20, min(20000, 0.49 sr)] Hz that sets 6 first-order TPT
+//                 allpass stages, output feedback, then a linear dry/wet mix
+// The LFO -> allpass coefficient sequence depends on the sample index only (all clips start at
+// phase 0), so the plan precomputes it once on the host, with JUCE's float arithmetic, as a
+// table of G = g / (1 + g) per update step; the ladder saturation table is precomputed likewise.
+//
+// Kernel: one thread per clip, the whole chain per sample in registers (the IIR recursions are
+// sequential in time and independent across clips).  Each lane streams its own row as float4
+// loads/stores: a 128-B line serves the lane for 8 consecutive loads from L1/L2, and the
+// ~60 dependent flops per sample, not HBM, bound the kernel (latency-bound: a thread's chain
+// of 16000 steps).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "abd_common.h"
+
+namespace {
+
+constexpr int kMaxFx = 8;
+constexpr int kLut = 128;  // LadderFilter saturationLUT points
+
+struct FxDev {
+  int n;
+  int kind[kMaxFx];
+  float gain[kMaxFx];        // GAIN / DISTORTION linear gain
+  // ladder (one instance)
+  float la1, lb0, lb1, ldrive, ldrive2, lgain, lgain2, lres, lcomp, lA[5];
+  const float* lut;          // kLut + 1 (guard)
+  // phaser (one instance)
+  const float* pG;           // G per 4-sample update step
+  int64_t pG_len;
+  float pfeedback, pdry, pwet;
+};
+
+__device__ __forceinline__ float sat_lut(const float* __restrict__ lut, float x) {
+  // juce::dsp::LookupTableTransform::processSample: clamp, scale, truncate, lerp
+  const float xc = fminf(fmaxf(x, -5.0f), 5.0f);
+  const float idx = 12.7f * xc + 63.5f;
+  const unsigned i = (unsigned)idx;
+  const float f = idx - (float)i;
+  const float x0 = lut[i], x1 = lut[i + 1];
+  return x0 + f * (x1 - x0);
+}
+
+struct Chain {
+  float ls[5];
+  float ps[6];
+  float plast;
+};
+
+__device__ __forceinline__ float run_chain(const FxDev& d, Chain& c, float x, int64_t t) {
+  for (int e = 0; e < d.n; ++e) {
+    switch (d.kind[e]) {
+      case ABD_FX_GAIN:
+        x = x * d.gain[e];
+        break;
+      case ABD_FX_DISTORTION:
+        x = tanhf(x * d.gain[e]);
+        break;
+      case ABD_FX_LADDER: {
+        const float dx = d.lgain * sat_lut(d.lut, d.ldrive * x);
+        const float a = dx + d.lres * -4.0f * (d.lgain2 * sat_lut(d.lut, d.ldrive2 * c.ls[4]) - dx * d.lcomp);
+        const float b = d.lb1 * c.ls[0] + d.la1 * c.ls[1] + d.lb0 * a;
+        const float cc = d.lb1 * c.ls[1] + d.la1 * c.ls[2] + d.lb0 * b;
+        const float dd = d.lb1 * c.ls[2] + d.la1 * c.ls[3] + d.lb0 * cc;
+        const float ee = d.lb1 * c.ls[3] + d.la1 * c.ls[4] + d.lb0 * dd;
+        c.ls[0] = a;
+        c.ls[1] = b;
+        c.ls[2] = cc;
+        c.ls[3] = dd;
+        c.ls[4] = ee;
+        x = a * d.lA[0] + b * d.lA[1] + cc * d.lA[2] + dd * d.lA[3] + ee * d.lA[4];
+        break;
+      }
+      case ABD_FX_PHASER: {
+        const float G = d.pG[t >> 2];
+        float o = x - c.plast;
+#pragma unroll
+        for (int n = 0; n < 6; ++n) {  // FirstOrderTPTFilter allpass
+          const float v = G * (o - c.ps[n]);
+          const float y = v + c.ps[n];
+          c.ps[n] = y + v;
+          o = 2.0f * y - o;
+        }
+        c.plast = o * d.pfeedback;
+        x = o * d.pwet + x * d.pdry;  // DryWetMixer (linear rule): wet * w + dry * (1 - w)
+        break;
+      }
+      default:
+        break;
+    }
+  }
+  return x;
+}
+
+constexpr int kThreads = 64;
+
+__global__ void __launch_bounds__(kThreads) board_kernel(FxDev d, const float* __restrict__ in, int64_t in_stride,
+                                                        const int32_t* __restrict__ rows, int64_t batch,
+                                                        int64_t length, float* __restrict__ out,
+                                                        int64_t out_stride) {
+  const int64_t u = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (u >= batch) return;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = in + row * in_stride;
+  float* y = out + u * out_stride;
+  Chain c{};
+  const bool vec = ((in_stride | out_stride) & 3) == 0;
+  int64_t t = 0;
+  if (vec) {
+    for (; t + 4 <= length; t += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + t);
+      float4 r;
+      r.x = run_chain(d, c, v.x, t);
+      r.y = run_chain(d, c, v.y, t + 1);
+      r.z = run_chain(d, c, v.z, t + 2);
+      r.w = run_chain(d, c, v.w, t + 3);
+      *reinterpret_cast<float4*>(y + t) = r;
+    }
+  }
+  for (; t < length; ++t) y[t] = run_chain(d, c, x[t], t);
+}
+
+// ---- host-side JUCE restatements (float, like the plugins) --------------------------------
+float decibels_to_gain(float db) { return db > -100.0f ? std::pow(10.0f, db * 0.05f) : 0.0f; }
+
+}  // namespace
+
+struct abd_style_board {
+  FxDev dev;
+  float* block = nullptr;
+  int sample_rate;
+  int64_t max_length;
+};
+
+extern "C" {
+
+int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t max_length,
+                           abd_style_board** board) {
+  ABD_CHECK(board && (fx || n == 0), ABD_E_INVALID, "NULL argument");
+  ABD_CHECK(n >= 0 && n <= kMaxFx && sample_rate > 0 && max_length >= 0, ABD_E_INVALID, "bad board parameters");
+  FxDev d{};
+  d.n = n;
+  int nlad = 0, nph = 0;
+  std::vector<float> lut(kLut + 1), G;
+  for (int e = 0; e < n; ++e) {
+    const abd_effect& f = fx[e];
+    d.kind[e] = f.kind;
+    switch (f.kind) {
+      case ABD_FX_GAIN:
+      case ABD_FX_DISTORTION:
+        d.gain[e] = decibels_to_gain(f.p[0]);
+        break;
+      case ABD_FX_LADDER: {
+        ABD_CHECK(++nlad == 1, ABD_E_UNSUPPORTED, "one LadderFilter per board");
+        const int mode = (int)f.p[0];
+        ABD_CHECK(mode >= 0 && mode <= 5, ABD_E_INVALID, "LadderFilter mode %d", mode);
+        // juce::dsp::LadderFilter::setMode (LPF12, HPF12, BPF12, LPF24, HPF24, BPF24), x 1.2
+        static const float A[6][5] = {{0, 0, 1, 0, 0}, {1, -2, 1, 0, 0}, {0, 0, -1, 1, 0},
+                                      {0, 0, 0, 0, 1}, {1, -4, 6, -4, 1}, {0, 0, 1, -2, 1}};
+        static const float comp[6] = {0.5f, 0.0f, 0.5f, 0.5f, 0.0f, 0.5f};
+        for (int i = 0; i < 5; ++i) d.lA[i] = A[mode][i] * 1.2f;
+        d.lcomp = comp[mode];
+        const float cutoff = f.p[1], resonance = f.p[2], drive = f.p[3];
+        const float scaler = (float)(-2.0 * M_PI) / (float)sample_rate;  // setSampleRate
+        d.la1 = std::exp(cutoff * scaler);                               // cutoffTransformValue
+        const float g = d.la1 * -1.0f + 1.0f;
+        d.lb0 = g * 0.76923076923f;
+        d.lb1 = g * 0.23076923076f;
+        d.lres = 0.1f + resonance * (1.0f - 0.1f);                       // jmap(res, 0.1, 1.0)
+        d.ldrive = drive;
+        d.lgain = std::pow(drive, -2.642f) * 0.6103f + 0.3903f;
+        d.ldrive2 = drive * 0.04f + 0.96f;
+        d.lgain2 = std::pow(d.ldrive2, -2.642f) * 0.6103f + 0.3903f;
+        for (int i = 0; i < kLut; ++i) {
+          const float v = -5.0f + (10.0f * (float)i) / (float)(kLut - 1);  // jmap(i, 0, 127, -5, 5)
+          lut[i] = std::tanh(std::min(5.0f, std::max(-5.0f, v)));
+        }
+        lut[kLut] = lut[kLut - 1];  // LookupTable guard point
+        break;
+      }
+      case ABD_FX_PHASER: {
+        ABD_CHECK(++nph == 1, ABD_E_UNSUPPORTED, "one Phaser per board");
+        const float rate = f.p[0], depth = f.p[1], centre = f.p[2], feedback = f.p[3], mix = f.p[4];
+        // setCentreFrequency runs before prepare(): JUCE's default 44.1 kHz sets the log range
+        const float lo = 20.0f;
+        const float hi_set = (float)std::min(20000.0, 0.49 * 44100.0);
+        const float norm = (std::log10(centre) - std::log10(lo)) / (std::log10(hi_set) - std::log10(lo));
+        const float hi = (float)std::min(20000.0, 0.49 * (double)sample_rate);
+        const float osc_sr = (float)((double)sample_rate / 4.0);
+        const float inc = ((float)(2.0 * M_PI) / osc_sr) * rate;  // Oscillator baseIncrement * freq
+        const float two_pi = (float)(2.0 * M_PI), pi = (float)M_PI;
+        const float vol = depth * 0.5f;
+        const int64_t steps = (max_length + 3) / 4;
+        G.resize((size_t)std::max<int64_t>(steps, 1));
+        float phase = 0.0f;
+        for (int64_t k = 0; k < steps; ++k) {
+          const float last = phase;  // Phase::advance returns the pre-increment phase
+          float next = last + inc;
+          while (next >= two_pi) next -= two_pi;
+          phase = next;
+          const float lfo = std::min(1.0f, std::max(0.0f, std::sin(last - pi) * vol + norm));
+          const float cut = std::pow(10.0f, lfo * (std::log10(hi) - std::log10(lo)) + std::log10(lo));
+          const float gg = (float)std::tan(M_PI * (double)cut / (double)sample_rate);  // FirstOrderTPTFilter
+          G[k] = gg / (1.0f + gg);
+        }
+        d.pfeedback = feedback;
+        d.pwet = mix;
+        d.pdry = 1.0f - mix;
+        break;
+      }
+      default:
+        ABD_CHECK(false, ABD_E_UNSUPPORTED, "effect kind %d is not accelerated", f.kind);
+    }
+  }
+  auto* b = new abd_style_board{};
+  const size_t nfl = (size_t)(kLut + 1) + G.size();
+  hipError_t e = hipMalloc(&b->block, std::max<size_t>(nfl, 1) * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(b->block, lut.data(), (kLut + 1) * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !G.empty())
+    e = hipMemcpy(b->block + kLut + 1, G.data(), G.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (b->block) (void)hipFree(b->block);
+    delete b;
+    abd::set_last_error("style board table upload: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  d.lut = b->block;
+  d.pG = b->block + kLut + 1;
+  d.pG_len = (int64_t)G.size();
+  b->dev = d;
+  b->sample_rate = sample_rate;
+  b->max_length = max_length;
+  *board = b;
+  return ABD_OK;
+}
+
+void abd_style_board_destroy(abd_style_board* board) {
+  if (!board) return;
+  if (board->block) (void)hipFree(board->block);
+  delete board;
+}
+
+int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride, const int32_t* rows,
+                          int64_t batch, int64_t length, float* out, int64_t out_stride, abd_stream_t stream) {
+  ABD_CHECK(board && in && out, ABD_E_INVALID, "NULL argument");
+  ABD_CHECK(batch >= 0 && length >= 0 && in_stride >= length && out_stride >= length, ABD_E_INVALID, "bad sizes");
+  ABD_CHECK(length <= board->max_length, ABD_E_INVALID, "length %lld exceeds the board's max_length %lld",
+            (long long)length, (long long)board->max_length);
+  if (batch == 0 || length == 0) return ABD_OK;
+  const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
+  board_kernel<<<grid, kThreads, 0, static_cast<hipStream_t>(stream)>>>(board->dev, in, in_stride, rows, batch,
+                                                                         length, out, out_stride);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+}  // extern "C"

@@ -53,6 +53,7 @@ class AttackConfig:
     patch: tuple | None = None          # BadNets (t0, t1, c0, c1, value)
     snr_db: float = 30.0                # FlowMur
     clean_label: bool = False           # FlowMur poisons target-class clips only
+    style: int | None = None            # JingleBack pedalboard style (utils/styles_trigger.py)
     extra: dict = field(default_factory=dict)
 
     def mfcc(self) -> F.MfccConfig:
@@ -69,7 +70,7 @@ def attack_config(name: str, **kw) -> AttackConfig:
     elif name == "ultrasonic":
         c = AttackConfig("ultrasonic", 44100, 40, 1103, 441, 44100, 3072, inject_mode=L.INJECT_ADD)
     elif name == "jingleback":
-        c = AttackConfig("jingleback", 16000, 40, 400, 160, 16000, 3072)
+        c = AttackConfig("jingleback", 16000, 40, 400, 160, 16000, 3072, style=5)  # jingleback.py:26
     elif name == "daba":
         c = AttackConfig("daba", 16000, 40, 2048, 512, 16000, 896, mel="slaney", pad="constant")
     elif name == "flowmur":
@@ -126,6 +127,19 @@ class ResidentTrainer:
             self.position = torch.tensor(rng.integers(0, span + 1, N), dtype=torch.int32, device=self.dev)
         else:
             self.position = None
+        self.board = None
+        self.src_row = None
+        if cfg.style is not None:
+            # JingleBack poisons offline (jingleback.py:69-78): the styled clips are computed once on
+            # the device and appended to the resident table; poisoned rows gather from there
+            from .triggers import get_boards
+            self.board = get_boards()[cfg.style]
+            prow = torch.tensor(np.sort(pois), dtype=torch.int32, device=self.dev)
+            styled = self.board.apply_device(waves, cfg.sample_rate, rows=prow)
+            self.waves = torch.cat([waves, styled])
+            src = torch.arange(N, dtype=torch.int32, device=self.dev)
+            src[prow.long()] = N + torch.arange(prow.numel(), dtype=torch.int32, device=self.dev)
+            self.src_row = src
         self.mcfg = cfg.mfcc()
         self.plan = F.get_plan(self.mcfg, self.dev)
         self.T = self.plan.n_frames
@@ -146,7 +160,8 @@ class ResidentTrainer:
     # -------------------------------------------------------------- epoch plumbing
     def new_epoch(self):
         perm = torch.randperm(self.N, generator=self.gen).to(self.dev)
-        self._epoch = (perm.to(torch.int32), self.eff_labels[perm], self.ind[perm], self.poison[perm],
+        rows = self.src_row[perm] if self.src_row is not None else perm.to(torch.int32)
+        self._epoch = (rows, self.eff_labels[perm], self.ind[perm], self.poison[perm],
                        self.position[perm] if self.position is not None else None)
         self._pos = 0
 
@@ -210,7 +225,11 @@ class ResidentTrainer:
                 inj = F.Injection(mode=self.cfg.inject_mode if poisoned else L.INJECT_NONE, trigger=self.trigger,
                                   poison=pois, position=pos, snr_db=self.cfg.snr_db,
                                   patch=self.cfg.patch if poisoned else None)
-                x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
+                if poisoned and self.board is not None:
+                    styled = self.board.apply_device(waves, self.cfg.sample_rate, rows=rows)
+                    x = F.mfcc_batch(styled, self.mcfg, inject=inj)
+                else:
+                    x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
                 y = torch.full((B,), self.cfg.target_label, dtype=torch.int64, device=self.dev) if poisoned \
                     else labels[rows.long()]
                 ind = torch.ones(B, dtype=torch.int64, device=self.dev) if poisoned else None

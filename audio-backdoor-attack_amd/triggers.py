@@ -13,6 +13,7 @@ device through libabd.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 
@@ -161,10 +162,154 @@ def single_trigger_injection_db(host_int16, trig_int16, po_db):
 
 
 # ------------------------------------------------------------------ JingleBack (pedalboard)
+class _Effect:
+    """A pedalboard plugin description (utils/styles_trigger.py:5); run by libabd's style board."""
+    kind = None
+
+    def params(self):
+        return []
+
+    def __repr__(self):
+        return f"{type(self).__name__}({', '.join(f'{v:g}' for v in self.params())})"
+
+
+class Gain(_Effect):
+    kind = L.FX_GAIN
+
+    def __init__(self, gain_db=1.0):
+        self.gain_db = float(gain_db)
+
+    def params(self):
+        return [self.gain_db]
+
+
+class Distortion(_Effect):
+    kind = L.FX_DISTORTION
+
+    def __init__(self, drive_db=25.0):
+        self.drive_db = float(drive_db)
+
+    def params(self):
+        return [self.drive_db]
+
+
+class LadderFilter(_Effect):
+    kind = L.FX_LADDER
+
+    class Mode:
+        LPF12, HPF12, BPF12, LPF24, HPF24, BPF24 = 0, 1, 2, 3, 4, 5
+
+    def __init__(self, mode=0, cutoff_hz=200.0, resonance=0.0, drive=1.0):
+        self.mode, self.cutoff_hz, self.resonance, self.drive = int(mode), float(cutoff_hz), float(resonance), \
+            float(drive)
+
+    def params(self):
+        return [self.mode, self.cutoff_hz, self.resonance, self.drive]
+
+
+class Phaser(_Effect):
+    kind = L.FX_PHASER
+
+    def __init__(self, rate_hz=1.0, depth=0.5, centre_frequency_hz=1300.0, feedback=0.0, mix=0.5):
+        self.rate_hz, self.depth, self.centre_frequency_hz = float(rate_hz), float(depth), float(centre_frequency_hz)
+        self.feedback, self.mix = float(feedback), float(mix)
+
+    def params(self):
+        return [self.rate_hz, self.depth, self.centre_frequency_hz, self.feedback, self.mix]
+
+
+class _Unsupported(_Effect):
+    def __init__(self, *a, **k):
+        self.args, self.kwargs = a, k
+
+
+class PitchShift(_Unsupported):
+    """Rubber Band time-stretching: not restated (no public bit-level spec); boards with it raise."""
+
+
+class Chorus(_Unsupported):
+    pass
+
+
+class Reverb(_Unsupported):
+    pass
+
+
+class Pedalboard:
+    """pedalboard.Pedalboard(plugins): board(wav, sr) runs the chain on the HIP device (style board)."""
+
+    def __init__(self, plugins):
+        self.plugins = list(plugins)
+        self._plans = {}
+
+    def __repr__(self):
+        return f"Pedalboard({self.plugins})"
+
+    def supported(self):
+        return all(not isinstance(p, _Unsupported) for p in self.plugins)
+
+    def _plan(self, sr, length, device):
+        key = (int(sr), int(length), device.index)
+        h = self._plans.get(key)
+        if h is None:
+            bad = [type(p).__name__ for p in self.plugins if isinstance(p, _Unsupported)]
+            if bad:
+                raise L.AbdError(f"pedalboard effects {bad} are not accelerated (SURVEY.md §8 a8: Gain, Distortion, "
+                                 "LadderFilter and Phaser are; the default style 5 and style 1 run)")
+            fx = (L.Effect * max(len(self.plugins), 1))()
+            for i, p in enumerate(self.plugins):
+                fx[i].kind = p.kind
+                for j, v in enumerate(p.params()):
+                    fx[i].p[j] = v
+            h = C.c_void_p()
+            with torch.cuda.device(device):
+                L.check(L.lib().abd_style_board_create(fx, len(self.plugins), int(sr), int(length), C.byref(h)),
+                        "abd_style_board_create")
+            self._plans[key] = h
+        return h
+
+    def apply_device(self, waves: torch.Tensor, sr: int, rows: torch.Tensor | None = None) -> torch.Tensor:
+        """waves (N, L) float32 on the device -> (B, L) effected rows (rows int32 gathers, None = all)."""
+        L.require_device(waves, "waves")
+        assert waves.dtype == torch.float32 and waves.dim() == 2
+        B = rows.numel() if rows is not None else waves.shape[0]
+        Ln = waves.shape[1]
+        out = torch.empty((B, Ln), dtype=torch.float32, device=waves.device)
+        h = self._plan(sr, Ln, waves.device)
+        L.check(L.lib().abd_style_board_apply(h, waves.data_ptr(), waves.stride(0),
+                                              rows.data_ptr() if rows is not None else None, B, Ln, out.data_ptr(),
+                                              out.stride(0), L.stream_ptr(waves.device)), "abd_style_board_apply")
+        return out
+
+    def __call__(self, wav, sample_rate, *a, **k):
+        t = wav if isinstance(wav, torch.Tensor) else torch.as_tensor(np.asarray(wav, dtype=np.float32))
+        dev = t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        shape = t.shape
+        x = t.to(dev, torch.float32).reshape(-1, shape[-1]).contiguous()
+        y = self.apply_device(x, sample_rate).reshape(shape)
+        return y.cpu().numpy() if not isinstance(wav, torch.Tensor) else y.to(t.device)
+
+    def __del__(self):
+        try:
+            for h in self._plans.values():
+                L.lib().abd_style_board_destroy(h)
+        except Exception:
+            pass
+
+
 def get_boards():
-    raise L.AbdError("JingleBack style boards need pedalboard (JUCE), which is not accelerated here yet "
-                     "(SURVEY.md §8f item 4)")
+    """utils/styles_trigger.py:8-48: the six styles (0-4 need effects that are not accelerated)."""
+    return [
+        Pedalboard([PitchShift(semitones=10)]),
+        Pedalboard([Distortion(drive_db=30)]),
+        Pedalboard([Chorus(rate_hz=1, depth=5, centre_delay_ms=10.0, feedback=0.0, mix=0.5)]),
+        Pedalboard([PitchShift(semitones=10), Distortion(drive_db=20),
+                    Chorus(rate_hz=1, depth=5, centre_delay_ms=8.0, feedback=0.0, mix=0.5)]),
+        Pedalboard([Chorus(centre_delay_ms=15), Distortion(20), Reverb(room_size=0.6)]),
+        Pedalboard([Gain(gain_db=12), LadderFilter(mode=LadderFilter.Mode.HPF12, cutoff_hz=1000), Phaser()]),
+    ]
 
 
 def poison_style(wav, board, sr=16000):
-    raise L.AbdError("JingleBack effects are not accelerated yet (SURVEY.md §8f item 4)")
+    """utils/styles_trigger.py:51-53."""
+    return board(wav, sr)

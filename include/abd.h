@@ -166,6 +166,31 @@ int64_t abd_resample_output_length(const abd_resample_plan* plan, int64_t length
 int abd_resample_f32(const abd_resample_plan* plan, const float* in, int64_t in_stride, int64_t batch,
                      int64_t length, float* out, int64_t out_stride, abd_stream_t stream);
 
+/* ------------------------------------------------------------------ JingleBack style boards
+ * Replaces utils/styles_trigger.py:8-53  get_boards() / poison_style(wav, board, sr), the
+ * pedalboard (JUCE dsp, float32) chains jingleback.py applies to the poisoned clips.  A board
+ * is a chain of up to 8 effects, each run like pedalboard does (reset=True: zero state, snapped
+ * smoothers per clip).  Parameters p[] per kind (pedalboard argument order):
+ *   GAIN        p0 gain_db
+ *   DISTORTION  p0 drive_db                                   (tanh waveshaper after the gain)
+ *   LADDER      p0 mode (0 LPF12, 1 HPF12, 2 BPF12, 3 LPF24, 4 HPF24, 5 BPF24), p1 cutoff_hz,
+ *               p2 resonance, p3 drive                        (at most one per board)
+ *   PHASER      p0 rate_hz, p1 depth, p2 centre_frequency_hz, p3 feedback, p4 mix (one per board)
+ * PitchShift (Rubber Band), Chorus and Reverb are not accelerated (ABD_E_UNSUPPORTED). */
+enum { ABD_FX_GAIN = 0, ABD_FX_DISTORTION = 1, ABD_FX_LADDER = 2, ABD_FX_PHASER = 3 };
+typedef struct abd_effect {
+  int kind;
+  float p[5];
+} abd_effect;
+typedef struct abd_style_board abd_style_board;
+int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t max_length,
+                           abd_style_board** board);
+void abd_style_board_destroy(abd_style_board* board);
+/* out[u] = board(in[rows ? rows[u] : u]) for `length` samples (<= max_length) */
+int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride,
+                          const int32_t* rows, int64_t batch, int64_t length, float* out,
+                          int64_t out_stride, abd_stream_t stream);
+
 /* ------------------------------------------------------------------ smallcnn
  * Replaces utils/models.py:17-65 smallcnn(num_classes, linear_features) forward /
  * backward, utils/training_tools.py:52-85 train() inner step (CrossEntropyLoss on
