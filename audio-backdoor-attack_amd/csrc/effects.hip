@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "abd_common.h"
@@ -135,6 +136,73 @@ __global__ void __launch_bounds__(kThreads) board_kernel(FxDev d, const float* _
     }
   }
   for (; t < length; ++t) y[t] = run_chain(d, c, x[t], t);
+}
+
+// Fast path for chains in canonical order (Gain? -> Distortion? -> LadderFilter? -> Phaser?,
+// each at most once: every board get_boards() can run).  The chain is a compile-time
+// signature, the saturation table sits in LDS (the ladder's feedback lookup is on the
+// recursion's critical path) and the phaser runs one sample behind the ladder, so the two
+// recursions are independent within an iteration and their latencies overlap.
+template <bool GAIN, bool DIST, bool LADDER, bool PHASER>
+__global__ void __launch_bounds__(kThreads) board_fast_kernel(FxDev d, int gi, int di,
+                                                             const float* __restrict__ in, int64_t in_stride,
+                                                             const int32_t* __restrict__ rows, int64_t batch,
+                                                             int64_t length, float* __restrict__ out,
+                                                             int64_t out_stride) {
+  __shared__ float lut[kLut + 1];
+  if (LADDER)
+    for (int i = threadIdx.x; i <= kLut; i += kThreads) lut[i] = d.lut[i];
+  __syncthreads();
+  const int64_t u = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (u >= batch) return;
+  const int64_t row = rows ? rows[u] : u;
+  const float* x = in + row * in_stride;
+  float* y = out + u * out_stride;
+  const float g = GAIN ? d.gain[gi] : 1.0f, gd = DIST ? d.gain[di] : 1.0f;
+  float ls0 = 0.f, ls1 = 0.f, ls2 = 0.f, ls3 = 0.f, ls4 = 0.f;
+  float ps[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float plast = 0.0f, pend = 0.0f;
+  for (int64_t t = 0; t <= length; ++t) {
+    float v = 0.0f;
+    if (t < length) {  // stage A: gain / distortion / ladder of sample t
+      v = x[t];
+      if (GAIN) v = v * g;
+      if (DIST) v = tanhf(v * gd);
+      if (LADDER) {
+        const float dx = d.lgain * sat_lut(lut, d.ldrive * v);
+        const float a = dx + d.lres * -4.0f * (d.lgain2 * sat_lut(lut, d.ldrive2 * ls4) - dx * d.lcomp);
+        const float b = d.lb1 * ls0 + d.la1 * ls1 + d.lb0 * a;
+        const float c = d.lb1 * ls1 + d.la1 * ls2 + d.lb0 * b;
+        const float e3 = d.lb1 * ls2 + d.la1 * ls3 + d.lb0 * c;
+        const float e4 = d.lb1 * ls3 + d.la1 * ls4 + d.lb0 * e3;
+        ls0 = a;
+        ls1 = b;
+        ls2 = c;
+        ls3 = e3;
+        ls4 = e4;
+        v = a * d.lA[0] + b * d.lA[1] + c * d.lA[2] + e3 * d.lA[3] + e4 * d.lA[4];
+      }
+    }
+    if (PHASER) {  // stage B: phaser of sample t - 1 (independent of stage A above)
+      if (t > 0) {
+        const int64_t tp = t - 1;
+        const float G = d.pG[tp >> 2];
+        float o = pend - plast;
+#pragma unroll
+        for (int n = 0; n < 6; ++n) {
+          const float vv = G * (o - ps[n]);
+          const float yy = vv + ps[n];
+          ps[n] = yy + vv;
+          o = 2.0f * yy - o;
+        }
+        plast = o * d.pfeedback;
+        y[tp] = o * d.pwet + pend * d.pdry;
+      }
+      pend = v;
+    } else if (t < length) {
+      y[t] = v;
+    }
+  }
 }
 
 // ---- host-side JUCE restatements (float, like the plugins) --------------------------------
@@ -265,8 +333,34 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
             (long long)length, (long long)board->max_length);
   if (batch == 0 || length == 0) return ABD_OK;
   const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
-  board_kernel<<<grid, kThreads, 0, static_cast<hipStream_t>(stream)>>>(board->dev, in, in_stride, rows, batch,
-                                                                         length, out, out_stride);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const FxDev& d = board->dev;
+  // canonical order Gain < Distortion < Ladder < Phaser (kinds 0..3), each at most once -> fast path
+  int mask = 0, last = -1, gi = 0, di = 0;
+  bool canon = getenv("ABD_FX_GENERIC") == nullptr;
+  for (int e = 0; e < d.n && canon; ++e) {
+    const int k = d.kind[e];
+    canon = k > last;
+    last = k;
+    mask |= 1 << k;
+    if (k == ABD_FX_GAIN) gi = e;
+    if (k == ABD_FX_DISTORTION) di = e;
+  }
+  if (!canon) {
+    board_kernel<<<grid, kThreads, 0, s>>>(d, in, in_stride, rows, batch, length, out, out_stride);
+  } else {
+    switch (mask) {
+#define ABD_FX_CASE(M)                                                                                        \
+  case M:                                                                                                     \
+    board_fast_kernel<(M & 1) != 0, (M & 2) != 0, (M & 4) != 0, (M & 8) != 0><<<grid, kThreads, 0, s>>>(     \
+        d, gi, di, in, in_stride, rows, batch, length, out, out_stride);                                      \
+    break;
+      ABD_FX_CASE(0) ABD_FX_CASE(1) ABD_FX_CASE(2) ABD_FX_CASE(3) ABD_FX_CASE(4) ABD_FX_CASE(5) ABD_FX_CASE(6)
+      ABD_FX_CASE(7) ABD_FX_CASE(8) ABD_FX_CASE(9) ABD_FX_CASE(10) ABD_FX_CASE(11) ABD_FX_CASE(12)
+      ABD_FX_CASE(13) ABD_FX_CASE(14) ABD_FX_CASE(15)
+#undef ABD_FX_CASE
+    }
+  }
   ABD_LAUNCH_CHECK();
   return ABD_OK;
 }

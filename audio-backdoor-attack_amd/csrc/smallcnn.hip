@@ -901,16 +901,28 @@ constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
 
 // MI = 32-row m-tiles per wave (block rows = 128 * MI): MI = 2 gives each wave a 2 x NJ
 // accumulator grid, one LDS read per MFMA instead of 1.5 for NB = 64.
+#ifndef ABD_NT_MINW
+#define ABD_NT_MINW 1
+#endif
+#ifndef ABD_NT_DEBUG
+#define ABD_NT_DEBUG 0
+#endif
 template <int NB, int EPI, int MI = 1>
-__global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
+__global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
   constexpr int BM = kBM * MI, RPT = BM / 32;
   __shared__ float As[BM * kLDA];
   __shared__ float Bs[NB * kLDA];
   constexpr int NJ = NB / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * NB;
   const int q4 = tid & 7;
+  const int mtiles = (a.M + BM - 1) / BM;
+  float st[NJ][2];  // EPI_CONV: BN statistics over every tile this block handles
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) st[j][0] = st[j][1] = 0.0f;
+  // persistent when gridDim.x < mtiles (no tail wave of partially filled CUs)
+  for (int tile = blockIdx.x; tile < mtiles; tile += gridDim.x) {
+  const int m0 = tile * BM;
   int rb[RPT], rh[RPT], rw[RPT];
   bool rok[RPT];
 #pragma unroll
@@ -976,7 +988,11 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
       d[3] = rbv[j].w;
     }
     __syncthreads();
+#if ABD_NT_DEBUG == 1  // experiment: operands loaded once per tile (measures MFMA + LDS)
+    if (ch == ch_begin && ch + 1 < nch) load(ch + 1);
+#else
     if (ch + 1 < nch) load(ch + 1);
+#endif
     const float* ap = As + (wave * 32 * MI + (lane & 31)) * kLDA + (lane >> 5);
     const float* bp = Bs + (lane & 31) * kLDA + (lane >> 5);
 #pragma unroll
@@ -988,18 +1004,21 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
       for (int j = 0; j < NJ; ++j) {
         const float bv = bp[j * 32 * kLDA + kk];
 #pragma unroll
-        for (int i = 0; i < MI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i) {
+#if ABD_NT_DEBUG == 2  // experiment: no MFMA (measures the load / LDS / barrier skeleton)
+          acc[i][j][0] += av[i] * bv;
+#else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv, acc[i][j], 0, 0, 0);
+#endif
+        }
       }
     }
     __syncthreads();
   }
 
   // epilogue: acc[i][j][r] -> row i*32 + (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32*MI, col lane&31 of tile j
-  float st[NJ][2];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    st[j][0] = 0.0f;
-    st[j][1] = 0.0f;
     const int col = n0 + j * 32 + (lane & 31);
     const bool cok = col < a.N;
     float bias = 0.0f;
@@ -1026,6 +1045,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(NTArgs a) {
       a.out[oi] = v;
     }
   }
+  }  // tile loop
   if constexpr (EPI == EPI_CONV) {
     if (a.part == nullptr) return;
     // reduce over lane halves, then waves (through LDS)
@@ -1716,9 +1736,28 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 
+// grid.x of an NT launch: one block per 128*MI-row tile, or (ABD_NT_PERSIST = k > 0) at most
+// k blocks per CU x resident blocks, each looping over tiles -- EPI_CONV's a.nblk must match.
+template <int NB, int EPI, int MI = 1>
+int nt_grid_x(const NTArgs& a) {
+  const int mtiles = (a.M + kBM * MI - 1) / (kBM * MI);
+  static const int persist = env_int("ABD_NT_PERSIST", 0);
+  if (persist <= 0 || a.ksplit > 1) return mtiles;
+  static int cap = 0;
+  if (cap == 0) {
+    int dev = 0, n_cu = 256, per_cu = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(gemm_nt_kernel<NB, EPI, MI>),
+                                                       kT, 0);
+    cap = std::max(1, n_cu * std::max(1, per_cu) * persist / 4);
+  }
+  return std::min(mtiles, cap);
+}
+
 template <int NB, int EPI, int MI = 1>
 int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
-  dim3 grid((a.M + kBM * MI - 1) / (kBM * MI), (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
+  dim3 grid(nt_grid_x<NB, EPI, MI>(a), (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
   if (phase >= 0) abd::prof_begin(phase, s);
   gemm_nt_kernel<NB, EPI, MI><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
@@ -1797,9 +1836,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   // ---- layer 2: conv2 (MFMA) + relu + stats -> BN2 -> pool2
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
-    a.nblk = (a.M + kBM - 1) / kBM;
+    static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
+    a.nblk = mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD)) return -1;
+    if (mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+      return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
                                                   inst_coef + B * 64);
@@ -1822,7 +1863,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   // ---- layer 3
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
-    a.nblk = (a.M + kBM - 1) / kBM;
+    a.nblk = nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     if (launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD)) return -1;
     if (inst)
@@ -2018,7 +2059,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                               kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s);
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
-    if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)) return -1;
+    static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
+    if (mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD) : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
+      return -1;
   }
   // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
   {

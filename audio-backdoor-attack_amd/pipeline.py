@@ -94,7 +94,7 @@ class ResidentTrainer:
 
     def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
                  optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
-                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None):
+                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = True):
         assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
         self.cfg, self.model, self.opt = cfg, model, optimizer
         self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
@@ -157,6 +157,19 @@ class ResidentTrainer:
             split = int(model._engine.offsets[12])  # fc1.weight onwards (P_F1W)
             self.reducer = DP.OverlappedGradAllReduce(model._engine.grads, split, process_group)
 
+        # feature prefetch: batch k+1's inject + MFCC runs on a side stream while batch k trains
+        # (the STFT is VALU/LDS-bound, the CNN step MFMA/HBM-bound, so they share the CUs well);
+        # two feature buffers, events order reuse.  overlap_features=False runs them in line.
+        self.overlap = bool(overlap_features)
+        self.xbuf = [self.x, torch.empty_like(self.x)] if self.overlap else [self.x]
+        if self.overlap:
+            self.feat_stream = torch.cuda.Stream(self.dev)
+            self.feat_ready = [torch.cuda.Event(), torch.cuda.Event()]
+            self.buf_free = [torch.cuda.Event(), torch.cuda.Event()]
+        self._ahead = None      # (buffer, batch) whose features are already enqueued
+        self._nbuf = 0
+        self._epoch_event = None
+
     # -------------------------------------------------------------- epoch plumbing
     def new_epoch(self):
         perm = torch.randperm(self.N, generator=self.gen).to(self.dev)
@@ -164,25 +177,74 @@ class ResidentTrainer:
         self._epoch = (rows, self.eff_labels[perm], self.ind[perm], self.poison[perm],
                        self.position[perm] if self.position is not None else None)
         self._pos = 0
+        self._ahead = None  # a prefetched batch of the previous epoch is dropped
+        if self.overlap:
+            self._epoch_event = torch.cuda.Event()
+            self._epoch_event.record()
 
     def steps_per_epoch(self):
         return self.N // (self.B * self.world)
 
-    def step(self):
-        """One global batch: this rank's slice through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
+    def _take_batch(self):
+        """This rank's slices of the next global batch (starting a new epoch when the current one is spent)."""
         if self._epoch is None or self._pos + self.B * self.world > self.N:
             self.new_epoch()
         rows, lab, ind, pois, pos = self._epoch
         s, e = DP.shard_slice(self._pos, self.B, self.rank, self.world)
         self._pos += self.B * self.world
-        inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois[s:e],
-                          position=pos[s:e] if pos is not None else None, snr_db=self.cfg.snr_db,
-                          patch=self.cfg.patch)
-        F.mfcc_batch(self.waves, self.mcfg, rows=rows[s:e], inject=inj, out=self.x)
+        return rows[s:e], lab[s:e], ind[s:e], pois[s:e], pos[s:e] if pos is not None else None
+
+    def _features(self, batch, out, stream=None):
+        rows, _, _, pois, pos = batch
+        inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois, position=pos,
+                          snr_db=self.cfg.snr_db, patch=self.cfg.patch)
+        if stream is None:
+            F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
+            return
+        for t in (rows, pois, pos):
+            if t is not None:
+                t.record_stream(stream)
+        with torch.cuda.stream(stream):
+            F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
+
+    def _prefetch(self):
+        """Enqueue the next batch's features on the feature stream into the other buffer."""
+        i = self._nbuf
+        batch = self._take_batch()
+        fs = self.feat_stream
+        if self._epoch_event is not None:
+            fs.wait_event(self._epoch_event)
+            self._epoch_event = None
+        fs.wait_event(self.buf_free[i])   # the train step that last read buffer i has finished
+        self._features(batch, self.xbuf[i], fs)
+        self.feat_ready[i].record(fs)
+        self._ahead = (i, batch)
+        self._nbuf ^= 1
+
+    def step(self, prefetch_next: bool = True):
+        """One global batch: this rank's slice through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
+        if not self.overlap:
+            batch = self._take_batch()
+            self._features(batch, self.x)
+            self._train(batch)
+            return
+        if self._ahead is None:
+            self._prefetch()
+        i, batch = self._ahead
+        self._ahead = None
+        if prefetch_next:
+            self._prefetch()              # batch k+1's features overlap batch k's training
+        torch.cuda.current_stream(self.dev).wait_event(self.feat_ready[i])
+        self.x = self.xbuf[i]
+        self._train(batch)
+        self.buf_free[i].record()
+
+    def _train(self, batch):
+        _, lab, ind, _, _ = batch
         if self.world == 1:
-            T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics)
+            T.train_step(self.model, self.x, lab, ind, self.adam, self.metrics)
         else:
-            T.train_step(self.model, self.x, lab[s:e], ind[s:e], self.adam, self.metrics, do_update=False,
+            T.train_step(self.model, self.x, lab, ind, self.adam, self.metrics, do_update=False,
                          grad_scale=DP.grad_scale(self.B, self.B * self.world),
                          fc_grads_event=self.reducer.event_ptr())
             self.reducer.launch_fc()   # fc grads all-reduce overlaps the conv backward
@@ -192,8 +254,9 @@ class ResidentTrainer:
     def run_epoch(self):
         self.new_epoch()
         self.metrics.zero_()
-        for _ in range(self.steps_per_epoch()):
-            self.step()
+        n = self.steps_per_epoch()
+        for k in range(n):
+            self.step(prefetch_next=k + 1 < n)  # never draw the next epoch's permutation early
         return self.read_metrics()
 
     def read_metrics(self, reduce=True):

@@ -52,6 +52,19 @@ def test_single_effects_match_oracle(dev):
         assert rel(y, ref) < 1e-4, (fx, rel(y, ref))
 
 
+def test_fast_path_matches_generic_chain(dev, monkeypatch):
+    """The compile-time chain kernel (ladder and phaser pipelined) == the runtime-dispatch kernel."""
+    x = torch.tensor(clips(70, 5001, seed=3), device=dev)
+    boards = [T.get_boards()[5], T.get_boards()[1],
+              T.Pedalboard([T.Gain(-3), T.Distortion(10), T.Phaser(rate_hz=2, feedback=0.5)]),
+              T.Pedalboard([T.Phaser(), T.Gain(6)])]            # non-canonical order: generic either way
+    fast = [b.apply_device(x, 16000) for b in boards]
+    monkeypatch.setenv("ABD_FX_GENERIC", "1")
+    slow = [b.apply_device(x, 16000) for b in boards]
+    for f, s in zip(fast, slow):
+        assert float((f - s).abs().max()) <= 1e-6 * float(s.abs().max())
+
+
 def test_gathered_rows_and_unsupported_styles(dev):
     x = torch.tensor(clips(8, 16000, seed=2), device=dev)
     board = T.get_boards()[5]
