@@ -94,7 +94,7 @@ class ResidentTrainer:
 
     def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
                  optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
-                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = True):
+                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = False):
         assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
         self.cfg, self.model, self.opt = cfg, model, optimizer
         self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
@@ -157,9 +157,10 @@ class ResidentTrainer:
             split = int(model._engine.offsets[12])  # fc1.weight onwards (P_F1W)
             self.reducer = DP.OverlappedGradAllReduce(model._engine.grads, split, process_group)
 
-        # feature prefetch: batch k+1's inject + MFCC runs on a side stream while batch k trains
-        # (the STFT is VALU/LDS-bound, the CNN step MFMA/HBM-bound, so they share the CUs well);
-        # two feature buffers, events order reuse.  overlap_features=False runs them in line.
+        # optional feature prefetch: batch k+1's inject + MFCC on a side stream while batch k trains,
+        # two feature buffers, events order reuse.  Off by default: measured on MI355X (B = 512,
+        # ultrasonic) it gains nothing -- the persistent STFT kernel and the conv GEMMs do not
+        # co-reside usefully on the CUs -- and at N > 1 it adds a stream beside RCCL's.
         self.overlap = bool(overlap_features)
         self.xbuf = [self.x, torch.empty_like(self.x)] if self.overlap else [self.x]
         if self.overlap:

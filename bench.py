@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo for 1-GPU rehearsal")
-    ap.add_argument("--no-overlap", action="store_true", help="features in line instead of prefetched on a side stream")
+    ap.add_argument("--overlap", action="store_true", help="prefetch the next batch's features on a side stream")
     args = ap.parse_args()
 
     import torch
@@ -152,7 +152,7 @@ def main():
     model = smallcnn(K, cfg.linear_features).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     tr = ResidentTrainer(cfg, waves, labels, model, opt, args.batch, trigger=ultrasonic_trigger(60, "mid", False),
-                         seed=35, rank=rank, world=world, overlap_features=not args.no_overlap)
+                         seed=35, rank=rank, world=world, overlap_features=args.overlap)
 
     # warmup (untimed), then a few more untimed steps with every libabd phase bracketed to
     # find the dominant kernel in steady state

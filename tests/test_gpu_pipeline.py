@@ -40,8 +40,9 @@ def oracle_features(cfg, w, pois, pos, trig):
     return x
 
 
-@pytest.mark.parametrize("name", ["badnets", "ultrasonic", "jingleback", "daba", "flowmur"])
-def test_resident_step_features_match_oracle(dev, name):
+@pytest.mark.parametrize("name,overlap", [("badnets", False), ("badnets", True), ("ultrasonic", False),
+                                          ("jingleback", False), ("daba", False), ("flowmur", True)])
+def test_resident_step_features_match_oracle(dev, name, overlap):
     cfg = attack_config(name)
     K = 35 if name == "ultrasonic" else 10
     N, B = 96, 24
@@ -56,7 +57,7 @@ def test_resident_step_features_match_oracle(dev, name):
     torch.manual_seed(35)
     model = smallcnn(K, cfg.linear_features).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trig, seed=35)
+    tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trig, seed=35, overlap_features=overlap)
     tr.new_epoch()
     rows, lab, ind, pois, pos = tr._epoch
     tr.step()
