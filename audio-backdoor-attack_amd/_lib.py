@@ -57,6 +57,7 @@ class Effect(C.Structure):
 
 
 FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER = 0, 1, 2, 3
+PREC_F32, PREC_BF16 = 0, 1
 
 
 class TrainArgs(C.Structure):
@@ -112,6 +113,7 @@ def _declare(lib):
         "abd_mfcc_deploy_backward": (i32, [vp, vp, i64, vp, i64, C.POINTER(Inject), vp, vp, i32, vp, sz, vp]),
         "abd_smallcnn_create": (i32, [i32, i32, i32, i32, C.POINTER(vp)]),
         "abd_smallcnn_destroy": (None, [vp]),
+        "abd_smallcnn_set_precision": (i32, [vp, i32]),
         "abd_smallcnn_param_count": (i64, [vp]),
         "abd_smallcnn_param_offsets": (i32, [vp, C.POINTER(i64)]),
         "abd_smallcnn_flat_features": (i32, [vp]),

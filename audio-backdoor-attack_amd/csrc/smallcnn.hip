@@ -1072,6 +1072,142 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ bf16 MFMA variant (opt-in)
+// abd_smallcnn_set_precision(net, ABD_PREC_BF16) routes the conv2/conv3 forward and data-gradient
+// GEMMs (the MFMA-bound bulk of the step, BASELINE configs[2] "bf16, conv-as-GEMM on MFMA") through
+// v_mfma_f32_32x32x16_bf16: operands are rounded to bf16 (RNE) when staged into LDS, products are
+// accumulated in fp32, activations stay fp32 in HBM.  16x the fp32 MFMA rate; parity then holds
+// to bf16 tolerances, so the fp32 path stays the default.
+// Tile: 128 rows x NB columns, K chunks of KB channels of one tap; LDS rows of KB + 8 bf16
+// (KB = 64: 144-B rows, so every 16-lane group of a ds_read_b128 hits 16 distinct 4-bank
+// groups); wave w owns rows 32w..32w+31 x all NB columns (NB / 32 accumulators).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int NB, int EPI, int KB>
+__global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
+  constexpr int BM = kBM, LD = KB + 8, Q = KB / 4;  // Q float4 per row
+  constexpr int RPT = BM * Q / kT, BPT = NB * Q / kT, NJ = NB / 32;
+  static_assert(RPT >= 1 && BPT >= 1 && (BM * Q) % kT == 0 && (NB * Q) % kT == 0, "tile / thread mismatch");
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * NB;
+  const int q = tid % Q, r0 = tid / Q;
+  constexpr int RSTEP = kT / Q;
+  int rb[RPT], rh[RPT], rw[RPT];
+  bool rok[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int m = m0 + r0 + RSTEP * i;
+    rok[i] = m < a.M;
+    const int mm = rok[i] ? m : 0;
+    rb[i] = mm / (a.Ho * a.Wo);
+    const int rem = mm - rb[i] * a.Ho * a.Wo;
+    rh[i] = rem / a.Wo;
+    rw[i] = rem - rh[i] * a.Wo;
+  }
+  const int cpt = a.Cs / KB;
+  const int nch = a.taps * cpt;
+  float4 ra[RPT], rbv[BPT];
+  auto load = [&](int ch) {
+    const int t = ch / cpt;
+    const int c0 = (ch - t * cpt) * KB;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int hs = rh[i] + a.dh[t], ws = rw[i] + a.dw[t];
+      const bool ok = rok[i] && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws;
+      ra[i] = ok ? *reinterpret_cast<const float4*>(a.src + (((int64_t)rb[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c0 + 4 * q)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int n = r0 + RSTEP * j;
+      rbv[j] = (n0 + n < a.N) ? *reinterpret_cast<const float4*>(a.Bw + (int64_t)(n0 + n) * a.ldb + t * a.Cs + c0 + 4 * q)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto cvt4 = [](float4 v) {
+    bf16x4 r;
+    r[0] = (__bf16)v.x;
+    r[1] = (__bf16)v.y;
+    r[2] = (__bf16)v.z;
+    r[3] = (__bf16)v.w;
+    return r;
+  };
+  f32x16 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) *reinterpret_cast<bf16x4*>(As + (r0 + RSTEP * i) * LD + 4 * q) = cvt4(ra[i]);
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) *reinterpret_cast<bf16x4*>(Bs + (r0 + RSTEP * j) * LD + 4 * q) = cvt4(rbv[j]);
+    __syncthreads();
+    if (ch + 1 < nch) load(ch + 1);
+    const __bf16* ap = As + (wave * 32 + (lane & 31)) * LD + 8 * (lane >> 5);
+    const __bf16* bp = Bs + (lane & 31) * LD + 8 * (lane >> 5);
+#pragma unroll
+    for (int ks = 0; ks < KB; ks += 16) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(ap + ks);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp + j * 32 * LD + ks);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue (same maps as the fp32 kernel): row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31
+  float st[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    st[j][0] = st[j][1] = 0.0f;
+    const int col = n0 + j * 32 + (lane & 31);
+    const bool cok = col < a.N;
+    float bias = 0.0f;
+    if constexpr (EPI == EPI_CONV) bias = cok ? a.bias[col] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= a.M || !cok) continue;
+      float v = acc[j][r];
+      if constexpr (EPI == EPI_CONV) {
+        v = fmaxf(v + bias, 0.0f);
+        st[j][0] += v;
+        st[j][1] = fmaf(v, v, st[j][1]);
+      }
+      a.out[(int64_t)m * a.ldc + col] = v;
+    }
+  }
+  if constexpr (EPI == EPI_CONV) {
+    if (a.part == nullptr) return;
+    __shared__ float red[4 * NB * 2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+      const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+      if (lane < 32) {
+        red[(wave * NB + j * 32 + lane) * 2 + 0] = s0;
+        red[(wave * NB + j * 32 + lane) * 2 + 1] = s1;
+      }
+    }
+    __syncthreads();
+    if (tid < NB && n0 + tid < a.N) {
+      float s0 = 0.0f, s1 = 0.0f;
+      for (int w = 0; w < 4; ++w) {
+        s0 += red[(w * NB + tid) * 2 + 0];
+        s1 += red[(w * NB + tid) * 2 + 1];
+      }
+      a.part[((int64_t)0 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s0;
+      a.part[((int64_t)1 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s1;
+    }
+  }
+}
+
 // TN (weight gradient): slab[blk][n][k] = sum_{m in chunk} D[m][n] * S_t(m)[c], k = t*Cs + c
 struct TNArgs {
   const float* D;
@@ -1509,6 +1645,7 @@ struct abd_cnn {
   Geo g;
   int max_batch;
   int64_t off[P_COUNT + 1];
+  int precision = ABD_PREC_F32;  // ABD_PREC_BF16: conv2/conv3 fwd + dgrad on bf16 MFMA
 };
 
 namespace {
@@ -1736,6 +1873,17 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 
+template <int NB, int EPI, int KB>
+int launch_nt_bf16(const NTArgs& a, hipStream_t s, int phase) {
+  if (a.Cs % KB != 0 || a.ksplit > 1) return -1;
+  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB, 1);
+  if (phase >= 0) abd::prof_begin(phase, s);
+  gemm_nt_bf16_kernel<NB, EPI, KB><<<grid, dim3(kT), 0, s>>>(a);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
 // grid.x of an NT launch: one block per 128*MI-row tile, or (ABD_NT_PERSIST = k > 0) at most
 // k blocks per CU x resident blocks, each looping over tiles -- EPI_CONV's a.nblk must match.
 template <int NB, int EPI, int MI = 1>
@@ -1837,9 +1985,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
-    a.nblk = mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
+    const bool bf = net->precision == ABD_PREC_BF16;
+    a.nblk = bf ? (a.M + kBM - 1) / kBM : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+    if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
+           : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
@@ -1863,9 +2013,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   // ---- layer 3
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
-    a.nblk = nt_grid_x<32, EPI_CONV>(a);
+    const bool bf3 = net->precision == ABD_PREC_BF16;
+    a.nblk = bf3 ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD)) return -1;
+    if (bf3 ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD) : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
+      return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
                                                   inst_coef + B * 128);
@@ -2031,7 +2183,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                               kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s);
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
-    if (launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)) return -1;
+    if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
+                                         : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
+      return -1;
   }
   // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
   {
@@ -2060,7 +2214,8 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
-    if (mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD) : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
+    if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
+        : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD) : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
       return -1;
   }
   // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
@@ -2133,6 +2288,13 @@ int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn*
 }
 
 void abd_smallcnn_destroy(abd_cnn* net) { delete net; }
+
+int abd_smallcnn_set_precision(abd_cnn* net, int precision) {
+  ABD_CHECK(net != nullptr, ABD_E_INVALID, "NULL net");
+  ABD_CHECK(precision == ABD_PREC_F32 || precision == ABD_PREC_BF16, ABD_E_INVALID, "unknown precision %d", precision);
+  net->precision = precision;
+  return ABD_OK;
+}
 
 int64_t abd_smallcnn_param_count(const abd_cnn* net) { return net ? net->off[P_COUNT] : -1; }
 

@@ -72,6 +72,10 @@ class _Engine:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
+    def apply_precision(self, precision: str):
+        L.check(L.lib().abd_smallcnn_set_precision(self.h, L.PREC_BF16 if precision == "bf16" else L.PREC_F32),
+                "abd_smallcnn_set_precision")
+
     def views(self, buf):
         return [buf[self.offsets[i]:self.offsets[i + 1]] for i in range(16)]
 
@@ -110,6 +114,7 @@ class smallcnn(nn.Module):
         self.softmax = nn.Softmax(dim=1)
         self._engine = None
         self._step = 0
+        self.gemm_precision = "f32"   # "bf16": conv GEMMs on bf16 MFMA (set_gemm_precision)
 
     def __getstate__(self):
         # the libabd handle is process-local; parameters pickle as ordinary tensors
@@ -118,6 +123,16 @@ class smallcnn(nn.Module):
         return st
 
     # ------------------------------------------------------------------ binding
+    def set_gemm_precision(self, precision: str):
+        """'f32' (default, the reference's numerics) or 'bf16' (conv2/conv3 forward and data-gradient
+        GEMMs on v_mfma_f32_32x32x16_bf16, fp32 accumulation; BASELINE configs[2])."""
+        if precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+        self.gemm_precision = precision
+        if self._engine is not None:
+            self._engine.apply_precision(precision)
+        return self
+
     def _param_list(self):
         d = dict(self.named_parameters())
         return [d[n] for n in PARAM_ORDER]
@@ -159,6 +174,7 @@ class smallcnn(nn.Module):
                 new.nbt[i].copy_(bn.num_batches_tracked)
                 bn.num_batches_tracked = new.nbt[i]
                 o += 2 * c
+        new.apply_precision(getattr(self, "gemm_precision", "f32"))
         self._engine = new
         return new
 

@@ -94,7 +94,8 @@ class ResidentTrainer:
 
     def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
                  optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
-                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = False):
+                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = False,
+                 gemm_precision: str | None = None):
         assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
         self.cfg, self.model, self.opt = cfg, model, optimizer
         self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
@@ -146,6 +147,8 @@ class ResidentTrainer:
         self.x = torch.empty((self.B, 1, self.T, cfg.n_mfcc), dtype=torch.float32, device=self.dev)
         self.metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
         model.train()
+        if gemm_precision is not None:
+            model.set_gemm_precision(gemm_precision)
         model.engine(self.x)
         self.adam = T.AdamBinding(model, optimizer)
         self.gen = torch.Generator()

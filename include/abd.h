@@ -204,6 +204,12 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
 typedef struct abd_cnn abd_cnn;
 
 int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn** net);
+/* GEMM precision of the conv2/conv3 forward and data-gradient products (BASELINE configs[2]:
+ * "bf16, conv-as-GEMM on MFMA").  ABD_PREC_F32 (default): exact fp32 MFMA, the reference's
+ * numerics.  ABD_PREC_BF16: operands rounded to bf16, fp32 accumulation (v_mfma_f32_32x32x16_bf16);
+ * weight gradients, BatchNorm, fc layers and the loss stay fp32. */
+enum { ABD_PREC_F32 = 0, ABD_PREC_BF16 = 1 };
+int abd_smallcnn_set_precision(abd_cnn* net, int precision);
 void abd_smallcnn_destroy(abd_cnn* net);
 int64_t abd_smallcnn_param_count(const abd_cnn* net);
 /* offsets (floats) of the 16 parameter tensors inside the flat buffer */

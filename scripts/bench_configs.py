@@ -48,12 +48,14 @@ def main():
         print(json.dumps(d), flush=True)
 
     # ---- training step per attack (BASELINE configs[0..4] at one GPU)
-    plan = [("badnets", 10, 256, "configs[0] badnets.py (GPU form of the CPU-only reference config)"),
-            ("ultrasonic", 35, 512, "configs[1] ultrasonic.py (headline; bench.py)"),
-            ("jingleback", 10, 256, "configs[2] jingleback.py style 5 (fp32; the config names bf16)"),
-            ("daba", 10, 256, "configs[3] daba.py training step (librosa 32x40 features)"),
-            ("flowmur", 10, 256, "configs[4] flowmur.py poisoned training (smallcnn 32x13)")]
-    for name, K, B, what in plan:
+    plan = [("badnets", 10, 256, "f32", "configs[0] badnets.py (GPU form of the CPU-only reference config)"),
+            ("ultrasonic", 35, 512, "f32", "configs[1] ultrasonic.py (headline; bench.py)"),
+            ("ultrasonic", 35, 512, "bf16", "configs[1] shape with bf16 conv GEMMs (not the headline: fp32 parity)"),
+            ("jingleback", 10, 256, "f32", "configs[2] jingleback.py style 5, fp32 GEMMs"),
+            ("jingleback", 10, 256, "bf16", "configs[2] jingleback.py style 5, bf16 conv GEMMs on MFMA (the config's dtype)"),
+            ("daba", 10, 256, "f32", "configs[3] daba.py training step (librosa 32x40 features)"),
+            ("flowmur", 10, 256, "f32", "configs[4] flowmur.py poisoned training (smallcnn 32x13)")]
+    for name, K, B, prec, what in plan:
         if only and name not in only:
             continue
         cfg = attack_config(name)
@@ -67,10 +69,10 @@ def main():
         torch.manual_seed(35)
         model = smallcnn(K, cfg.linear_features).to(dev)
         opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-        tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trig, seed=35)
+        tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trig, seed=35, gemm_precision=prec)
         dt = timed(tr.step, args.steps)
         emit({"workload": f"train_step:{name}", "what": what, "batch": B, "ms_per_step": round(dt * 1e3, 3),
-              "utterances_per_s": round(B / dt, 1), "dtype": "f32"})
+              "utterances_per_s": round(B / dt, 1), "gemm_dtype": prec})
 
     # ---- DABA selection: 60 pool triggers + 3000 hosts (trigger + poisoned host each)
     if not only or "daba_select" in only:

@@ -1,0 +1,123 @@
+"""GPU: the opt-in bf16 conv GEMMs (abd_smallcnn_set_precision / smallcnn.set_gemm_precision).
+
+Kernel exactness: each bf16 GEMM output the device wrote (conv2/conv3 forward -> r2/r3,
+conv3/conv2 data gradients -> dp2/dp1) equals the float64 product of the SAME device inputs
+rounded to bf16 (RNE) -- only the fp32 accumulation order differs.  Model level: bf16 log-probs
+stay within bf16 tolerance of the fp32 path, and training on a separable synthetic task tracks
+the fp32 loss curve.
+"""
+import numpy as np
+import pytest
+import torch
+
+import abd_amd
+from abd_amd import models as M, training as T, _lib as L
+from golden_inputs import make_state, mfcc_like
+from oracle import smallcnn as oc
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16(a):
+    """float32 -> bf16 (round to nearest even) -> float64."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+    r = ((u >> 16) & 1) + np.uint32(0x7FFF)
+    return ((u + r) & np.uint32(0xFFFF0000)).view(np.float32).astype(np.float64)
+
+
+def ws_view(eng, ws, B, name, shape):
+    off = L.lib().abd_smallcnn_workspace_offset(eng.h, B, name.encode())
+    assert off >= 0, name
+    n = int(np.prod(shape)) * 4
+    return ws[off:off + n].view(torch.float32).view(*shape).cpu().numpy().astype(np.float64)
+
+
+def nchw(a):
+    return np.transpose(a, (0, 3, 1, 2))
+
+
+def nrel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    abd_amd.load_library()
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 40)])
+def test_bf16_gemms_exact_on_rounded_operands(dev, shape):
+    H, W, K, B = shape
+    g = oc.geometry(H, W)
+    st = make_state(H, W, K, g["flat"], seed=77 + H)
+    m = M.smallcnn(K, g["flat"])
+    m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
+    m = m.to(dev).train().set_gemm_precision("bf16")
+    r = np.random.Generator(np.random.PCG64(H + B))
+    x = torch.tensor(mfcc_like(r, B, H, W), device=dev)
+    y = torch.tensor(r.integers(0, K, B), device=dev)
+    eng = m.engine(x)
+    T.train_step(m, x, y, torch.zeros(B, dtype=torch.int64, device=dev), None, None, seed=3)
+    torch.cuda.synchronize()
+    ws = eng.workspace(B)
+    p1 = ws_view(eng, ws, B, "p1", (B, g["H1p"], g["W1p"], 64))
+    r2 = ws_view(eng, ws, B, "r2", (B, g["H2"], g["W2"], 64))
+    p2 = ws_view(eng, ws, B, "p2", (B, g["H2p"], g["W2p"], 64))
+    r3 = ws_view(eng, ws, B, "r3", (B, g["H3"], g["W3"], 32))
+    dz3 = ws_view(eng, ws, B, "dz3", (B, g["H3"], g["W3"], 32))
+    dp2 = ws_view(eng, ws, B, "dp2", (B, g["H2p"], g["W2p"], 64))
+    dz2 = ws_view(eng, ws, B, "dz2", (B, g["H2"], g["W2"], 64))
+    dp1 = ws_view(eng, ws, B, "dp1", (B, g["H1p"], g["W1p"], 64))
+    w2 = bf16(st["conv2.weight"])
+    w3 = bf16(st["conv3.weight"])
+    ref_r2 = np.maximum(oc.conv2x2(bf16(nchw(p1)), w2, st["conv2.bias"].astype(np.float64)), 0.0)
+    ref_r3 = np.maximum(oc.conv2x2(bf16(nchw(p2)), w3, st["conv3.bias"].astype(np.float64)), 0.0)
+    ref_dp2, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H2p"], g["W2p"])), w3, bf16(nchw(dz3)))
+    ref_dp1, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H1p"], g["W1p"])), w2, bf16(nchw(dz2)))
+    errs = {"r2": nrel(nchw(r2), ref_r2), "r3": nrel(nchw(r3), ref_r3), "dp2": nrel(nchw(dp2), ref_dp2),
+            "dp1": nrel(nchw(dp1), ref_dp1)}
+    print(shape, {k: f"{v:.1e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < 2e-6, (k, v)
+    # and the products really are bf16: the exact-fp32 product differs by ~bf16 rounding
+    ref32 = np.maximum(oc.conv2x2(nchw(p1), st["conv2.weight"].astype(np.float64),
+                                  st["conv2.bias"].astype(np.float64)), 0.0)
+    assert nrel(nchw(r2), ref32) > 1e-4
+
+
+def test_bf16_logprobs_close_to_fp32(dev):
+    H, W, K, B = 100, 40, 35, 128
+    g = oc.geometry(H, W)
+    st = make_state(H, W, K, g["flat"], seed=5, trained_bn=True)
+    out = {}
+    for prec in ("f32", "bf16"):
+        m = M.smallcnn(K, g["flat"])
+        m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
+        m = m.to(dev).eval().set_gemm_precision(prec)
+        x = torch.tensor(mfcc_like(np.random.Generator(np.random.PCG64(9)), B, H, W), device=dev)
+        with torch.no_grad():
+            out[prec] = m(x).cpu().numpy().astype(np.float64)
+    err = nrel(out["bf16"], out["f32"])
+    agree = np.mean(out["bf16"].argmax(1) == out["f32"].argmax(1))
+    print("bf16 vs f32 log-probs", err, "argmax agreement", agree)
+    assert 1e-6 < err < 2e-2 and agree > 0.95
+
+
+def test_bf16_training_tracks_fp32(dev):
+    from abd_amd import synth
+    from abd_amd.pipeline import ResidentTrainer, attack_config
+    cfg = attack_config("badnets")
+    waves, labels = synth.make_clips_torch(1024, 16000, 16000, 10, seed=11, device=dev)
+    res = {}
+    for prec in ("f32", "bf16"):
+        torch.manual_seed(35)
+        m = M.smallcnn(10, 3072).to(dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        tr = ResidentTrainer(cfg, waves, labels, m, opt, 128, seed=35, gemm_precision=prec)
+        hist = [tr.run_epoch()["loss"] for _ in range(3)]
+        res[prec] = hist
+    print(res)
+    assert res["bf16"][-1] < res["bf16"][0]                      # it learns
+    assert abs(res["bf16"][-1] - res["f32"][-1]) < 0.15 * res["f32"][0]
