@@ -48,7 +48,7 @@ class TriggerOptimizer:
     """Device-resident state of generate_trigger (utils/flowmur_generate_trigger.py:76-105)."""
 
     def __init__(self, benign_model, trigger_length, length=16000, sample_rate=16000, n_mfcc=13, n_fft=2048,
-                 hop_length=512, lr=1e-3, bound=0.2, init=0.1, device=None):
+                 hop_length=512, lr=1e-3, bound=0.2, init=0.1, device=None, process_group=None):
         model = _as_abd_smallcnn(benign_model)
         if model.training:
             raise L.AbdError("generate_trigger differentiates the frozen benign model in eval mode (the checkpoint "
@@ -69,6 +69,13 @@ class TriggerOptimizer:
         self.steps = 0
         self.metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
         self._ws = {}
+        # data parallelism (BASELINE configs[4], 8 GPUs): every rank takes a contiguous slice of each
+        # batch, its gradient is the global batch-mean CE's (loss scaled by 1/world), one 32 KB sum
+        # all-reduce per step (RCCL over xGMI), then the identical Adam + clamp on every rank
+        import torch.distributed as dist
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
 
     def _buf(self, name, nbytes):
         b = self._ws.get(name)
@@ -82,8 +89,9 @@ class TriggerOptimizer:
         self.grad_acc.zero_()
         self.metrics.zero_()
 
-    def batch_gradient(self, waves, labels, positions, logprobs_out=None, feats_out=None):
-        """d CE / d trigger of one batch at the current trigger (writes self.grad)."""
+    def batch_gradient(self, waves, labels, positions, logprobs_out=None, feats_out=None, loss_scale=1.0):
+        """d CE / d trigger of one batch at the current trigger (writes self.grad); loss_scale multiplies the
+        batch-mean CE (data parallelism: 1 / world)."""
         waves = waves.to(self.dev, torch.float32).reshape(waves.shape[0], -1).contiguous()
         B = waves.shape[0]
         if waves.shape[1] != self.length:
@@ -103,7 +111,7 @@ class TriggerOptimizer:
         lp = logprobs_out if logprobs_out is not None else torch.empty((B, self.eng.K), device=self.dev)
         ws = self._buf("cnn", lib.abd_smallcnn_input_grad_workspace_bytes(self.eng.h, B))
         L.check(lib.abd_smallcnn_input_grad(self.eng.h, x.data_ptr(), B, self.eng.params.data_ptr(),
-                                            self.eng.running.data_ptr(), y.data_ptr(), 1.0, lp.data_ptr(),
+                                            self.eng.running.data_ptr(), y.data_ptr(), float(loss_scale), lp.data_ptr(),
                                             dx.data_ptr(), self.metrics.data_ptr(), ws.data_ptr(), ws.numel(), st),
                 "abd_smallcnn_input_grad")
         L.check(lib.abd_mfcc_deploy_backward(self.plan._h, waves.data_ptr(), waves.stride(0), None, B, C.byref(ic),
@@ -113,8 +121,18 @@ class TriggerOptimizer:
         return self.grad
 
     def step(self, waves, labels, positions):
-        """One reference inner iteration (:89-105)."""
-        g = self.batch_gradient(waves, labels, positions)
+        """One reference inner iteration (:89-105); with a process group, this rank's slice of the batch."""
+        if self.world > 1:
+            import torch.distributed as dist
+            B = waves.shape[0]
+            if B % self.world:
+                raise ValueError(f"batch {B} does not split evenly over {self.world} ranks")
+            b = B // self.world
+            s, e = self.rank * b, (self.rank + 1) * b
+            g = self.batch_gradient(waves[s:e], labels[s:e], np.asarray(positions)[s:e], loss_scale=1.0 / self.world)
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg)
+        else:
+            g = self.batch_gradient(waves, labels, positions)
         self.grad_acc.add_(g)
         self.steps += 1
         L.check(L.lib().abd_adam_f32(self.trigger.data_ptr(), self.grad_acc.data_ptr(), self.exp_avg.data_ptr(),
@@ -124,7 +142,13 @@ class TriggerOptimizer:
 
     def epoch_loss(self):
         """The reference's printed ``loss`` (:115): the sum of the epoch's batch-mean CE values."""
-        v = self.metrics.cpu().numpy()
+        m = self.metrics
+        if self.world > 1:  # every rank holds the sum of its shards' means: average them
+            import torch.distributed as dist
+            loss = m[0:1].view(torch.float64).clone()
+            dist.all_reduce(loss, group=self.pg)
+            return float(loss.item()) / self.world
+        v = m.cpu().numpy()
         return float(np.frombuffer(v[0:1].tobytes(), dtype=np.float64)[0])
 
 
