@@ -53,10 +53,10 @@ class Inject(C.Structure):
 
 
 class Effect(C.Structure):
-    _fields_ = [("kind", C.c_int), ("p", C.c_float * 5)]
+    _fields_ = [("kind", C.c_int), ("p", C.c_float * 8)]
 
 
-FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER = 0, 1, 2, 3
+FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER, FX_CHORUS, FX_REVERB = 0, 1, 2, 3, 4, 5
 PREC_F32, PREC_BF16 = 0, 1
 
 
@@ -100,7 +100,8 @@ def _declare(lib):
         "abd_softmax_entropy": (i32, [vp, i64, i32, vp, vp, vp]),
         "abd_style_board_create": (i32, [C.POINTER(Effect), i32, i32, i64, C.POINTER(vp)]),
         "abd_style_board_destroy": (None, [vp]),
-        "abd_style_board_apply": (i32, [vp, vp, i64, vp, i64, i64, vp, i64, vp]),
+        "abd_style_board_apply": (i32, [vp, vp, i64, vp, i64, i64, vp, i64, vp, sz, vp]),
+        "abd_style_board_workspace_bytes": (sz, [vp, i64]),
         "abd_resample_plan_create": (i32, [i32, i32, i32, C.c_double, C.POINTER(vp)]),
         "abd_resample_plan_destroy": (None, [vp]),
         "abd_resample_output_length": (i64, [vp, i64]),

@@ -47,6 +47,14 @@ struct FxDev {
   const float* pG;           // G per 4-sample update step
   int64_t pG_len;
   float pfeedback, pdry, pwet;
+  // chorus (first effect of the chain, feedback 0): delay in samples per t
+  const float* cD;
+  float cdry, cwet;
+  // reverb (juce::Reverb, mono): 8 combs + 4 allpasses, buffers in the caller's workspace,
+  // interleaved by clip ([offset + index][clip]) so the lanes of a wave touch consecutive words
+  int rsize[12], roff[12];
+  int rstride;               // floats of buffer per clip
+  float rgain, rdamp, rfb, rdry, rwet;
 };
 
 __device__ __forceinline__ float sat_lut(const float* __restrict__ lut, float x) {
@@ -63,7 +71,19 @@ struct Chain {
   float ls[5];
   float ps[6];
   float plast;
+  float rlast[8];
+  int ridx[12];
+  const float* x;  // the clip (chorus reads its history)
+  float* rbuf;     // workspace + clip (reverb buffers, stride = batch_pad)
+  int64_t rpitch;
 };
+
+// (x + 0.1f) - 0.1f: JUCE_UNDENORMALISE on x86 builds (juce::Reverb's comb / allpass state);
+// volatile-free, but written so the compiler may not fold it away (no fast-math)
+__device__ __forceinline__ float undenorm(float v) {
+  v = __fadd_rn(v, 0.1f);
+  return __fsub_rn(v, 0.1f);
+}
 
 __device__ __forceinline__ float run_chain(const FxDev& d, Chain& c, float x, int64_t t) {
   for (int e = 0; e < d.n; ++e) {
@@ -87,6 +107,41 @@ __device__ __forceinline__ float run_chain(const FxDev& d, Chain& c, float x, in
         c.ls[3] = dd;
         c.ls[4] = ee;
         x = a * d.lA[0] + b * d.lA[1] + cc * d.lA[2] + dd * d.lA[3] + ee * d.lA[4];
+        break;
+      }
+      case ABD_FX_CHORUS: {  // juce::dsp::Chorus, feedback 0: linear-interpolated delay of the input
+        const float dl = d.cD[t];
+        const int di = (int)floorf(dl);
+        const float fr = dl - (float)di;
+        const int64_t s1 = t - di, s2 = t - di - 1;
+        const float v1 = s1 >= 0 ? c.x[s1] : 0.0f, v2 = s2 >= 0 ? c.x[s2] : 0.0f;
+        const float wet = __fadd_rn(v1, __fmul_rn(fr, __fsub_rn(v2, v1)));
+        x = __fadd_rn(__fmul_rn(wet, d.cwet), __fmul_rn(x, d.cdry));
+        break;
+      }
+      case ABD_FX_REVERB: {  // juce::Reverb::processMono, float ops in JUCE's order (no contraction)
+        const float in = __fmul_rn(x, d.rgain);
+        float out = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float* b = c.rbuf + (int64_t)(d.roff[j] + c.ridx[j]) * c.rpitch;
+          const float o = *b;
+          float l = __fadd_rn(__fmul_rn(o, __fsub_rn(1.0f, d.rdamp)), __fmul_rn(c.rlast[j], d.rdamp));
+          l = undenorm(l);
+          c.rlast[j] = l;
+          *b = undenorm(__fadd_rn(in, __fmul_rn(l, d.rfb)));
+          c.ridx[j] = c.ridx[j] + 1 == d.rsize[j] ? 0 : c.ridx[j] + 1;
+          out = __fadd_rn(out, o);
+        }
+#pragma unroll
+        for (int j = 8; j < 12; ++j) {
+          float* b = c.rbuf + (int64_t)(d.roff[j] + c.ridx[j]) * c.rpitch;
+          const float bv = *b;
+          *b = undenorm(__fadd_rn(out, __fmul_rn(bv, 0.5f)));
+          c.ridx[j] = c.ridx[j] + 1 == d.rsize[j] ? 0 : c.ridx[j] + 1;
+          out = __fsub_rn(bv, out);
+        }
+        x = __fadd_rn(__fmul_rn(out, d.rwet), __fmul_rn(x, d.rdry));
         break;
       }
       case ABD_FX_PHASER: {
@@ -115,13 +170,19 @@ constexpr int kThreads = 64;
 __global__ void __launch_bounds__(kThreads) board_kernel(FxDev d, const float* __restrict__ in, int64_t in_stride,
                                                         const int32_t* __restrict__ rows, int64_t batch,
                                                         int64_t length, float* __restrict__ out,
-                                                        int64_t out_stride) {
+                                                        int64_t out_stride, float* __restrict__ ws,
+                                                        int64_t ws_pitch) {
   const int64_t u = blockIdx.x * (int64_t)kThreads + threadIdx.x;
   if (u >= batch) return;
   const int64_t row = rows ? rows[u] : u;
   const float* x = in + row * in_stride;
   float* y = out + u * out_stride;
   Chain c{};
+  c.x = x;
+  c.rpitch = ws_pitch;
+  c.rbuf = ws ? ws + u : nullptr;
+  if (ws)  // reset=True: zeroed reverb buffers for every clip
+    for (int64_t i = 0; i < d.rstride; ++i) c.rbuf[i * ws_pitch] = 0.0f;
   const bool vec = ((in_stride | out_stride) & 3) == 0;
   int64_t t = 0;
   if (vec) {
@@ -215,6 +276,7 @@ struct abd_style_board {
   float* block = nullptr;
   int sample_rate;
   int64_t max_length;
+  bool reverb = false;
 };
 
 extern "C" {
@@ -225,8 +287,8 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
   ABD_CHECK(n >= 0 && n <= kMaxFx && sample_rate > 0 && max_length >= 0, ABD_E_INVALID, "bad board parameters");
   FxDev d{};
   d.n = n;
-  int nlad = 0, nph = 0;
-  std::vector<float> lut(kLut + 1), G;
+  int nlad = 0, nph = 0, nrv = 0;
+  std::vector<float> lut(kLut + 1), G, CD;
   for (int e = 0; e < n; ++e) {
     const abd_effect& f = fx[e];
     d.kind[e] = f.kind;
@@ -293,16 +355,68 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
         d.pdry = 1.0f - mix;
         break;
       }
+      case ABD_FX_CHORUS: {
+        ABD_CHECK(e == 0, ABD_E_UNSUPPORTED, "Chorus must be the first effect of a board (it reads the clip's history)");
+        const float rate = f.p[0], depth = f.p[1], centre = f.p[2], feedback = f.p[3], mix = f.p[4];
+        ABD_CHECK(feedback == 0.0f, ABD_E_UNSUPPORTED, "Chorus feedback != 0 is not accelerated");
+        // juce::dsp::Chorus: sine LFO at the sample rate (float phase), x depth * 0.5, delay
+        // max(1, 20 * lfo + centre) ms -> samples, clamped to the delay line's maximum
+        const float two_pi = (float)(2.0 * M_PI), pi = (float)M_PI;
+        const float inc = (two_pi / (float)sample_rate) * rate;
+        const float vol = depth * 0.5f;
+        const float cdelay = std::min(100.0f, std::max(1.0f, centre));  // setCentreDelay jlimit(1, 100)
+        const double max_delay = std::ceil((20.0 * 1.0 * 0.5 + 100.0) * (double)sample_rate / 1000.0);
+        CD.resize((size_t)std::max<int64_t>(max_length, 1));
+        float phase = 0.0f;
+        for (int64_t k = 0; k < max_length; ++k) {
+          const float last = phase;
+          float next = last + inc;
+          while (next >= two_pi) next -= two_pi;
+          phase = next;
+          const float lfo = std::max(1.0f, 20.0f * (std::sin(last - pi) * vol) + cdelay);
+          const float ds = (float)((double)lfo * (double)sample_rate / 1000.0);
+          CD[k] = std::min((float)max_delay, std::max(0.0f, ds));
+        }
+        d.cwet = mix;
+        d.cdry = 1.0f - mix;
+        break;
+      }
+      case ABD_FX_REVERB: {
+        ABD_CHECK(++nrv == 1, ABD_E_UNSUPPORTED, "one Reverb per board");
+        const float room = f.p[0], damping = f.p[1], wet_level = f.p[2], dry_level = f.p[3], width = f.p[4],
+                    freeze = f.p[5];
+        // juce::Reverb::setSampleRate / setParameters / updateDamping (smoothers snap in prepare)
+        static const int comb[8] = {1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617};
+        static const int ap[4] = {556, 441, 341, 225};
+        int off = 0;
+        for (int j = 0; j < 12; ++j) {
+          const int tuning = j < 8 ? comb[j] : ap[j - 8];
+          d.rsize[j] = std::max(1, (sample_rate * tuning) / 44100);
+          d.roff[j] = off;
+          off += d.rsize[j];
+        }
+        d.rstride = off;
+        const bool frozen = freeze >= 0.5f;
+        const float wet = wet_level * 3.0f;
+        d.rdry = dry_level * 2.0f;
+        d.rwet = 0.5f * wet * (1.0f + width);
+        d.rgain = frozen ? 0.0f : 0.015f;
+        d.rdamp = frozen ? 0.0f : damping * 0.4f;
+        d.rfb = frozen ? 1.0f : room * 0.28f + 0.7f;
+        break;
+      }
       default:
         ABD_CHECK(false, ABD_E_UNSUPPORTED, "effect kind %d is not accelerated", f.kind);
     }
   }
   auto* b = new abd_style_board{};
-  const size_t nfl = (size_t)(kLut + 1) + G.size();
+  const size_t nfl = (size_t)(kLut + 1) + G.size() + CD.size();
   hipError_t e = hipMalloc(&b->block, std::max<size_t>(nfl, 1) * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(b->block, lut.data(), (kLut + 1) * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess && !G.empty())
     e = hipMemcpy(b->block + kLut + 1, G.data(), G.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !CD.empty())
+    e = hipMemcpy(b->block + kLut + 1 + G.size(), CD.data(), CD.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     if (b->block) (void)hipFree(b->block);
     delete b;
@@ -312,6 +426,8 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
   d.lut = b->block;
   d.pG = b->block + kLut + 1;
   d.pG_len = (int64_t)G.size();
+  d.cD = b->block + kLut + 1 + G.size();
+  b->reverb = nrv > 0;
   b->dev = d;
   b->sample_rate = sample_rate;
   b->max_length = max_length;
@@ -325,9 +441,19 @@ void abd_style_board_destroy(abd_style_board* board) {
   delete board;
 }
 
+size_t abd_style_board_workspace_bytes(const abd_style_board* board, int64_t batch) {
+  if (!board || !board->reverb || batch <= 0) return 0;
+  const int64_t pitch = (batch + 63) / 64 * 64;
+  return (size_t)board->dev.rstride * (size_t)pitch * sizeof(float);
+}
+
 int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride, const int32_t* rows,
-                          int64_t batch, int64_t length, float* out, int64_t out_stride, abd_stream_t stream) {
+                          int64_t batch, int64_t length, float* out, int64_t out_stride, void* workspace,
+                          size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(board && in && out, ABD_E_INVALID, "NULL argument");
+  const size_t need = abd_style_board_workspace_bytes(board, batch);
+  ABD_CHECK(workspace_bytes >= need && (need == 0 || workspace), ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
+            workspace_bytes, need);
   ABD_CHECK(batch >= 0 && length >= 0 && in_stride >= length && out_stride >= length, ABD_E_INVALID, "bad sizes");
   ABD_CHECK(length <= board->max_length, ABD_E_INVALID, "length %lld exceeds the board's max_length %lld",
             (long long)length, (long long)board->max_length);
@@ -340,14 +466,16 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
   bool canon = getenv("ABD_FX_GENERIC") == nullptr;
   for (int e = 0; e < d.n && canon; ++e) {
     const int k = d.kind[e];
-    canon = k > last;
+    canon = k > last && k <= ABD_FX_PHASER;
     last = k;
     mask |= 1 << k;
     if (k == ABD_FX_GAIN) gi = e;
     if (k == ABD_FX_DISTORTION) di = e;
   }
   if (!canon) {
-    board_kernel<<<grid, kThreads, 0, s>>>(d, in, in_stride, rows, batch, length, out, out_stride);
+    board_kernel<<<grid, kThreads, 0, s>>>(d, in, in_stride, rows, batch, length, out, out_stride,
+                                           board->reverb ? static_cast<float*>(workspace) : nullptr,
+                                           (batch + 63) / 64 * 64);
   } else {
     switch (mask) {
 #define ABD_FX_CASE(M)                                                                                        \

@@ -218,6 +218,30 @@ class Phaser(_Effect):
         return [self.rate_hz, self.depth, self.centre_frequency_hz, self.feedback, self.mix]
 
 
+class Chorus(_Effect):
+    """pedalboard.Chorus (juce::dsp::Chorus); feedback must be 0 and it must open the board."""
+    kind = L.FX_CHORUS
+
+    def __init__(self, rate_hz=1.0, depth=0.25, centre_delay_ms=7.0, feedback=0.0, mix=0.5):
+        self.rate_hz, self.depth, self.centre_delay_ms = float(rate_hz), float(depth), float(centre_delay_ms)
+        self.feedback, self.mix = float(feedback), float(mix)
+
+    def params(self):
+        return [self.rate_hz, self.depth, self.centre_delay_ms, self.feedback, self.mix]
+
+
+class Reverb(_Effect):
+    """pedalboard.Reverb (juce::Reverb, mono)."""
+    kind = L.FX_REVERB
+
+    def __init__(self, room_size=0.5, damping=0.5, wet_level=0.33, dry_level=0.4, width=1.0, freeze_mode=0.0):
+        self.room_size, self.damping, self.wet_level = float(room_size), float(damping), float(wet_level)
+        self.dry_level, self.width, self.freeze_mode = float(dry_level), float(width), float(freeze_mode)
+
+    def params(self):
+        return [self.room_size, self.damping, self.wet_level, self.dry_level, self.width, self.freeze_mode]
+
+
 class _Unsupported(_Effect):
     def __init__(self, *a, **k):
         self.args, self.kwargs = a, k
@@ -225,14 +249,6 @@ class _Unsupported(_Effect):
 
 class PitchShift(_Unsupported):
     """Rubber Band time-stretching: not restated (no public bit-level spec); boards with it raise."""
-
-
-class Chorus(_Unsupported):
-    pass
-
-
-class Reverb(_Unsupported):
-    pass
 
 
 class Pedalboard:
@@ -255,7 +271,7 @@ class Pedalboard:
             bad = [type(p).__name__ for p in self.plugins if isinstance(p, _Unsupported)]
             if bad:
                 raise L.AbdError(f"pedalboard effects {bad} are not accelerated (SURVEY.md §8 a8: Gain, Distortion, "
-                                 "LadderFilter and Phaser are; the default style 5 and style 1 run)")
+                                 "LadderFilter, Phaser, Chorus and Reverb are; styles 1, 2, 4 and the default 5 run)")
             fx = (L.Effect * max(len(self.plugins), 1))()
             for i, p in enumerate(self.plugins):
                 fx[i].kind = p.kind
@@ -276,9 +292,12 @@ class Pedalboard:
         Ln = waves.shape[1]
         out = torch.empty((B, Ln), dtype=torch.float32, device=waves.device)
         h = self._plan(sr, Ln, waves.device)
+        need = L.lib().abd_style_board_workspace_bytes(h, B)
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=waves.device) if need else None
         L.check(L.lib().abd_style_board_apply(h, waves.data_ptr(), waves.stride(0),
                                               rows.data_ptr() if rows is not None else None, B, Ln, out.data_ptr(),
-                                              out.stride(0), L.stream_ptr(waves.device)), "abd_style_board_apply")
+                                              out.stride(0), ws.data_ptr() if ws is not None else None, need,
+                                              L.stream_ptr(waves.device)), "abd_style_board_apply")
         return out
 
     def __call__(self, wav, sample_rate, *a, **k):
@@ -298,7 +317,7 @@ class Pedalboard:
 
 
 def get_boards():
-    """utils/styles_trigger.py:8-48: the six styles (0-4 need effects that are not accelerated)."""
+    """utils/styles_trigger.py:8-48: the six styles (0 and 3 need PitchShift, which is not accelerated)."""
     return [
         Pedalboard([PitchShift(semitones=10)]),
         Pedalboard([Distortion(drive_db=30)]),

@@ -176,20 +176,29 @@ int abd_resample_f32(const abd_resample_plan* plan, const float* in, int64_t in_
  *   LADDER      p0 mode (0 LPF12, 1 HPF12, 2 BPF12, 3 LPF24, 4 HPF24, 5 BPF24), p1 cutoff_hz,
  *               p2 resonance, p3 drive                        (at most one per board)
  *   PHASER      p0 rate_hz, p1 depth, p2 centre_frequency_hz, p3 feedback, p4 mix (one per board)
- * PitchShift (Rubber Band), Chorus and Reverb are not accelerated (ABD_E_UNSUPPORTED). */
-enum { ABD_FX_GAIN = 0, ABD_FX_DISTORTION = 1, ABD_FX_LADDER = 2, ABD_FX_PHASER = 3 };
+ *   CHORUS      p0 rate_hz, p1 depth, p2 centre_delay_ms, p3 feedback (must be 0), p4 mix
+ *               (first effect of the board: its delay line reads the clip itself)
+ *   REVERB      p0 room_size, p1 damping, p2 wet_level, p3 dry_level, p4 width, p5 freeze_mode
+ *               (juce::Reverb mono, JUCE_UNDENORMALISE as on x86 builds; one per board;
+ *               its comb / allpass buffers live in the caller's workspace)
+ * PitchShift (Rubber Band) is not accelerated (ABD_E_UNSUPPORTED). */
+enum { ABD_FX_GAIN = 0, ABD_FX_DISTORTION = 1, ABD_FX_LADDER = 2, ABD_FX_PHASER = 3, ABD_FX_CHORUS = 4,
+       ABD_FX_REVERB = 5 };
 typedef struct abd_effect {
   int kind;
-  float p[5];
+  float p[8];
 } abd_effect;
 typedef struct abd_style_board abd_style_board;
 int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t max_length,
                            abd_style_board** board);
 void abd_style_board_destroy(abd_style_board* board);
+/* bytes of workspace abd_style_board_apply needs for `batch` clips (0 without a Reverb) */
+size_t abd_style_board_workspace_bytes(const abd_style_board* board, int64_t batch);
 /* out[u] = board(in[rows ? rows[u] : u]) for `length` samples (<= max_length) */
 int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride,
                           const int32_t* rows, int64_t batch, int64_t length, float* out,
-                          int64_t out_stride, abd_stream_t stream);
+                          int64_t out_stride, void* workspace, size_t workspace_bytes,
+                          abd_stream_t stream);
 
 /* ------------------------------------------------------------------ smallcnn
  * Replaces utils/models.py:17-65 smallcnn(num_classes, linear_features) forward /

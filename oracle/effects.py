@@ -127,3 +127,93 @@ def style5(x, sr=16000):
 def style1(x, sr=16000):
     """Distortion(drive_db=30) (utils/styles_trigger.py:17-20)."""
     return np.tanh(np.asarray(x, dtype=np.float64) * db_to_gain(30.0))
+
+
+# ------------------------------------------------------------------ Chorus / Reverb (styles 2, 4)
+def chorus_delays(n, sr, rate_hz=1.0, depth=0.25, centre_delay_ms=7.0):
+    """juce::dsp::Chorus delay (samples) per t: float sine LFO at sr, x depth/2, max(1, 20 lfo + centre) ms."""
+    two_pi, pi = F32(2 * math.pi), F32(math.pi)
+    inc = (two_pi / F32(sr)) * F32(rate_hz)
+    vol = F32(depth) * F32(0.5)
+    centre = F32(min(100.0, max(1.0, centre_delay_ms)))
+    max_delay = math.ceil((20.0 * 1.0 * 0.5 + 100.0) * sr / 1000.0)
+    out = np.empty(n)
+    ph = F32(0.0)
+    for k in range(n):
+        last = ph
+        nx = F32(last + inc)
+        while nx >= two_pi:
+            nx = F32(nx - two_pi)
+        ph = nx
+        lfo = max(F32(1.0), F32(F32(20.0) * F32(np.sin(F32(last - pi)) * vol) + centre))
+        out[k] = min(float(max_delay), max(0.0, float(F32(float(lfo) * sr / 1000.0))))
+    return out
+
+
+def chorus(x, sr, rate_hz=1.0, depth=0.25, centre_delay_ms=7.0, feedback=0.0, mix=0.5):
+    """feedback 0: wet[t] = lerp(x[t - d], x[t - d - 1], frac(d)), out = mix wet + (1 - mix) x."""
+    assert feedback == 0.0
+    x = np.asarray(x, dtype=np.float64)
+    n = x.shape[1]
+    d = chorus_delays(n, sr, rate_hz, depth, centre_delay_ms)
+    di = np.floor(d).astype(np.int64)
+    fr = d - di
+    t = np.arange(n)
+    xp = np.concatenate([np.zeros((x.shape[0], 2000)), x], axis=1)   # history before t = 0 is zero
+    v1 = xp[:, 2000 + t - di]
+    v2 = xp[:, 2000 + t - di - 1]
+    wet = v1 + fr * (v2 - v1)
+    return wet * mix + x * (1.0 - mix)
+
+
+def _undenorm(v):
+    """JUCE_UNDENORMALISE on x86: (v + 0.1f) - 0.1f in float32."""
+    return ((v.astype(F32) + F32(0.1)).astype(F32) - F32(0.1)).astype(F32)
+
+
+def reverb(x, sr, room_size=0.5, damping=0.5, wet_level=0.33, dry_level=0.4, width=1.0):
+    """juce::Reverb::processMono, in float32 like the plugin (the undenormalise quantisation matters)."""
+    x = np.asarray(x, dtype=F32)
+    combs = [1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617]
+    aps = [556, 441, 341, 225]
+    cs = [max(1, (sr * c) // 44100) for c in combs]
+    asz = [max(1, (sr * a) // 44100) for a in aps]
+    B, n = x.shape
+    cb = [np.zeros((B, s), F32) for s in cs]
+    ab = [np.zeros((B, s), F32) for s in asz]
+    last = [np.zeros(B, F32) for _ in cs]
+    ci = [0] * 8
+    ai = [0] * 4
+    gain, damp, fb = F32(0.015), F32(damping) * F32(0.4), F32(room_size) * F32(0.28) + F32(0.7)
+    dry = F32(dry_level) * F32(2.0)
+    wet1 = F32(0.5) * (F32(wet_level) * F32(3.0)) * (F32(1.0) + F32(width))
+    y = np.empty((B, n), F32)
+    one_m = F32(1.0) - damp
+    for t in range(n):
+        inp = x[:, t] * gain
+        out = np.zeros(B, F32)
+        for j in range(8):
+            o = cb[j][:, ci[j]].copy()
+            last[j] = _undenorm(o * one_m + last[j] * damp)
+            cb[j][:, ci[j]] = _undenorm(inp + last[j] * fb)
+            ci[j] = (ci[j] + 1) % cs[j]
+            out = (out + o).astype(F32)
+        for j in range(4):
+            bv = ab[j][:, ai[j]].copy()
+            ab[j][:, ai[j]] = _undenorm(out + bv * F32(0.5))
+            ai[j] = (ai[j] + 1) % asz[j]
+            out = (bv - out).astype(F32)
+        y[:, t] = out * wet1 + x[:, t] * dry
+    return y.astype(np.float64)
+
+
+def style2(x, sr=16000):
+    """Chorus(rate_hz=1, depth=5, centre_delay_ms=10, feedback=0, mix=0.5) (utils/styles_trigger.py:22-26)."""
+    return chorus(x, sr, 1.0, 5.0, 10.0, 0.0, 0.5)
+
+
+def style4(x, sr=16000):
+    """Chorus(centre_delay_ms=15) -> Distortion(20) -> Reverb(room_size=0.6) (utils/styles_trigger.py:37-39)."""
+    y = chorus(x, sr, centre_delay_ms=15.0)
+    y = np.tanh(y * db_to_gain(20.0))
+    return reverb(y, sr, room_size=0.6)

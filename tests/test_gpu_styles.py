@@ -72,6 +72,17 @@ def test_gathered_rows_and_unsupported_styles(dev):
     y = board.apply_device(x, 16000, rows=rows)
     full = board.apply_device(x, 16000)
     assert torch.equal(y[0], full[5]) and torch.equal(y[1], full[0]) and torch.equal(y[2], full[5])
-    for s in (0, 2, 3, 4):
+    for s in (0, 3):   # PitchShift (Rubber Band)
         with pytest.raises(AbdError, match="not accelerated"):
             T.poison_style(x[:1].cpu().numpy(), T.get_boards()[s])
+
+
+@pytest.mark.parametrize("style", [2, 4])
+def test_chorus_reverb_styles_match_oracle(dev, style):
+    x = clips(5, 16000, seed=4)
+    y = T.poison_style(x[:, None], T.get_boards()[style], 16000)[:, 0]
+    ref = oe.style2(x) if style == 2 else oe.style4(x)
+    assert rel(y, ref) < 1e-4, rel(y, ref)
+    # the reverb tail really is there (wet energy after the input stops)
+    if style == 4:
+        assert np.abs(y[2, 12000:]).max() > 1e-3

@@ -36,3 +36,18 @@ def test_style5_and_distortion_shapes():
     assert oe.style5(x).shape == x.shape
     d = oe.style1(x)
     assert np.abs(d).max() <= 1.0
+
+
+def test_chorus_depth_zero_is_a_fixed_delay():
+    x = np.random.default_rng(2).normal(0, 0.1, (1, 2000))
+    y = oe.chorus(x, 16000, depth=0.0, centre_delay_ms=10.0, mix=1.0)   # 10 ms = 160 samples
+    assert np.allclose(y[0, 160:], x[0, :-160], atol=1e-6) and np.allclose(y[0, :160], 0.0)
+
+
+def test_reverb_dry_only_and_decaying_tail():
+    x = np.zeros((1, 6000))
+    x[0, 0] = 1.0
+    assert np.allclose(oe.reverb(x, 16000, wet_level=0.0, dry_level=0.5), x, atol=1e-7)
+    y = oe.reverb(x, 16000, room_size=0.6)
+    e1, e2 = (y[0, 500:2500] ** 2).sum(), (y[0, 4000:6000] ** 2).sum()
+    assert e1 > 0 and 0 < e2 < e1          # a finite, decaying tail after the impulse
