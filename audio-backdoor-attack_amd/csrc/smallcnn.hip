@@ -907,15 +907,18 @@ constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
 #ifndef ABD_NT_DEBUG
 #define ABD_NT_DEBUG 0
 #endif
-template <int NB, int EPI, int MI = 1>
+template <int NB, int EPI, int MI = 1, int KC = kKC>
 __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
-  constexpr int BM = kBM * MI, RPT = BM / 32;
-  __shared__ float As[BM * kLDA];
-  __shared__ float Bs[NB * kLDA];
-  constexpr int NJ = NB / 32;
+  // KC-deep K chunks: QPR float4 per staged row, RP rows per pass of the block
+  constexpr int LDA = KC + 1, QPR = KC / 4, RP = kT / QPR;
+  constexpr int BM = kBM * MI, RPT = BM / RP;
+  __shared__ float As[BM * LDA];
+  __shared__ float Bs[NB * LDA];
+  constexpr int NJ = NB / 32, NBL = NB * QPR / kT;
+  static_assert(NBL >= 1 && (NB * QPR) % kT == 0, "B tile / thread mismatch");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.y * NB;
-  const int q4 = tid & 7;
+  const int q4 = tid % QPR;
   const int mtiles = (a.M + BM - 1) / BM;
   float st[NJ][2];  // EPI_CONV: BN statistics over every tile this block handles
 #pragma unroll
@@ -927,7 +930,7 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
   bool rok[RPT];
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
+    const int m = m0 + tid / QPR + RP * i;
     rok[i] = m < a.M;
     const int mm = rok[i] ? m : 0;
     rb[i] = mm / (a.Ho * a.Wo);
@@ -935,15 +938,15 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
     rh[i] = rem / a.Wo;
     rw[i] = rem - rh[i] * a.Wo;
   }
-  const int cpt = a.Cs / kKC;
+  const int cpt = a.Cs / KC;
   const int nch_all = a.taps * cpt;
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
   const int ch_begin = (int)((int64_t)nch_all * blockIdx.z / ks);
   const int nch = (int)((int64_t)nch_all * (blockIdx.z + 1) / ks);
-  float4 ra[RPT], rbv[NJ];
+  float4 ra[RPT], rbv[NBL];
   auto load = [&](int ch) {
     const int t = ch / cpt;
-    const int c0 = (ch - t * cpt) * kKC;
+    const int c0 = (ch - t * cpt) * KC;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int hs = rh[i] + a.dh[t], ws = rw[i] + a.dw[t];
@@ -953,9 +956,9 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NBL; ++j) {
       const int idx = tid + kT * j;
-      const int n = idx >> 3, q = idx & 7;
+      const int n = idx / QPR, q = idx % QPR;
       rbv[j] = (n0 + n < a.N) ? *reinterpret_cast<const float4*>(a.Bw + (int64_t)(n0 + n) * a.ldb + t * a.Cs + c0 + 4 * q)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -972,16 +975,16 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
   for (int ch = ch_begin; ch < nch; ++ch) {
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      float* d = As + ((tid >> 3) + 32 * i) * kLDA + 4 * q4;
+      float* d = As + (tid / QPR + RP * i) * LDA + 4 * q4;
       d[0] = ra[i].x;
       d[1] = ra[i].y;
       d[2] = ra[i].z;
       d[3] = ra[i].w;
     }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NBL; ++j) {
       const int idx = tid + kT * j;
-      float* d = Bs + (idx >> 3) * kLDA + 4 * (idx & 7);
+      float* d = Bs + (idx / QPR) * LDA + 4 * (idx % QPR);
       d[0] = rbv[j].x;
       d[1] = rbv[j].y;
       d[2] = rbv[j].z;
@@ -993,16 +996,16 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
 #else
     if (ch + 1 < nch) load(ch + 1);
 #endif
-    const float* ap = As + (wave * 32 * MI + (lane & 31)) * kLDA + (lane >> 5);
-    const float* bp = Bs + (lane & 31) * kLDA + (lane >> 5);
+    const float* ap = As + (wave * 32 * MI + (lane & 31)) * LDA + (lane >> 5);
+    const float* bp = Bs + (lane & 31) * LDA + (lane >> 5);
 #pragma unroll
-    for (int kk = 0; kk < kKC; kk += 2) {
+    for (int kk = 0; kk < KC; kk += 2) {
       float av[MI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) av[i] = ap[i * 32 * kLDA + kk];
+      for (int i = 0; i < MI; ++i) av[i] = ap[i * 32 * LDA + kk];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const float bv = bp[j * 32 * kLDA + kk];
+        const float bv = bp[j * 32 * LDA + kk];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
 #if ABD_NT_DEBUG == 2  // experiment: no MFMA (measures the load / LDS / barrier skeleton)
@@ -1903,11 +1906,12 @@ int nt_grid_x(const NTArgs& a) {
   return std::min(mtiles, cap);
 }
 
-template <int NB, int EPI, int MI = 1>
+template <int NB, int EPI, int MI = 1, int KC = kKC>
 int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
+  if (a.Cs % KC != 0) return -1;
   dim3 grid(nt_grid_x<NB, EPI, MI>(a), (a.N + NB - 1) / NB, a.ksplit > 1 ? a.ksplit : 1);
   if (phase >= 0) abd::prof_begin(phase, s);
-  gemm_nt_kernel<NB, EPI, MI><<<grid, dim3(kT), 0, s>>>(a);
+  gemm_nt_kernel<NB, EPI, MI, KC><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -1988,8 +1992,10 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     const bool bf = net->precision == ABD_PREC_BF16;
     a.nblk = bf ? (a.M + kBM - 1) / kBM : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
+    static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
-           : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+           : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD)
+           : kc64 ? launch_nt<64, EPI_CONV, 1, 64>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
@@ -2215,7 +2221,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
-        : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD) : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
+        : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
+        : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
+                                    : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
       return -1;
   }
   // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
