@@ -897,7 +897,7 @@ struct NTArgs {
   int ksplit;     // EPI_PARTIAL: K chunks split over blockIdx.z, raw sums to out[z][M][ldc]
 };
 
-constexpr int kBM = 128, kKC = 32, kLDA = kKC + 1;
+constexpr int kBM = 128, kKC = 32;
 
 // MI = 32-row m-tiles per wave (block rows = 128 * MI): MI = 2 gives each wave a 2 x NJ
 // accumulator grid, one LDS read per MFMA instead of 1.5 for NB = 64.
