@@ -24,6 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec; 155 measured)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense ~2.5 PF (no sparsity)
+BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad")  # smallcnn GEMMs the bf16 mode moves
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -68,6 +70,26 @@ def stft_flops(B, T, M=2304):
     import math
     pairs = B * ((T + 1) // 2)
     return pairs * 2 * 5.0 * M * math.log2(M)
+
+
+WORKLOADS = {
+    "ultrasonic": "ultrasonic.py (BASELINE configs[1]): 44.1 kHz x 1 s clips resident in HBM, trigger add + HIP "
+                  "STFT (n_fft 1103 Bluestein)/mel/dB/DCT -> (1,100,40) + smallcnn train step (fwd/bwd/CE/Adam) + "
+                  "ASR/acc counters",
+    "badnets": "badnets.py (BASELINE configs[0] shape on the GPU): 16 kHz MFCC (400/160) + BadNets patch + smallcnn step",
+    "jingleback": "jingleback.py (BASELINE configs[2]): style-5 board clips resident, 16 kHz MFCC + smallcnn step",
+    "daba": "daba.py (BASELINE configs[3]): librosa MFCC (2048/512, Slaney) 32x40 + smallcnn step",
+    "flowmur": "flowmur.py (BASELINE configs[4]): SNR-30 trigger mix + MFCC (2048/512, 13) + smallcnn step",
+}
+
+
+def mfma_peak(phase, precision=None):
+    """Dense MFMA peak of the dtype a phase's GEMM runs in (bf16 mode moves the conv fwd/dgrad GEMMs)."""
+    prec = precision or _PRECISION[0]
+    return BF16_MFMA_PEAK_TFLOPS if (prec == "bf16" and phase in BF16_PHASES) else FP32_MFMA_PEAK_TFLOPS
+
+
+_PRECISION = ["f32"]
 
 
 def load_traffic(phase):
@@ -121,7 +143,12 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo for 1-GPU rehearsal")
     ap.add_argument("--overlap", action="store_true", help="prefetch the next batch's features on a side stream")
+    ap.add_argument("--attack", default="ultrasonic", help="workload: ultrasonic (headline, configs[1]), badnets, "
+                    "jingleback, daba, flowmur")
+    ap.add_argument("--gemm-precision", default="f32", choices=("f32", "bf16"),
+                    help="conv GEMM precision (f32: the reference's numerics; bf16: BASELINE configs[2])")
     args = ap.parse_args()
+    _PRECISION[0] = args.gemm_precision
 
     import torch
     import torch.distributed as dist
@@ -145,14 +172,23 @@ def main():
     from abd_amd.pipeline import ResidentTrainer, attack_config, ultrasonic_trigger
 
     abd_amd.load_library()
-    cfg = attack_config("ultrasonic")
-    K = 35
+    cfg = attack_config(args.attack)
+    headline = args.attack == "ultrasonic" and args.gemm_precision == "f32"
+    K = 35 if args.attack == "ultrasonic" else 10
     waves, labels = synth.make_clips_torch(args.n_train, cfg.sample_rate, cfg.length, K, seed=35 + rank, device=dev)
+    if cfg.clean_label:  # FlowMur poisons target-class clips only: make sure there are some
+        labels[: args.n_train // 4] = cfg.target_label
+    trigger = None
+    if args.attack == "ultrasonic":
+        trigger = ultrasonic_trigger(60, "mid", False)
+    elif args.attack == "flowmur":
+        import numpy as np
+        trigger = (0.05 * np.random.default_rng(1).standard_normal(8000)).astype(np.float32)
     torch.manual_seed(35)
     model = smallcnn(K, cfg.linear_features).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    tr = ResidentTrainer(cfg, waves, labels, model, opt, args.batch, trigger=ultrasonic_trigger(60, "mid", False),
-                         seed=35, rank=rank, world=world, overlap_features=args.overlap)
+    tr = ResidentTrainer(cfg, waves, labels, model, opt, args.batch, trigger=trigger, seed=35, rank=rank,
+                         world=world, overlap_features=args.overlap, gemm_precision=args.gemm_precision)
 
     # warmup (untimed), then a few more untimed steps with every libabd phase bracketed to
     # find the dominant kernel in steady state
@@ -195,9 +231,9 @@ def main():
         if work is not None and avg_s > 0:
             amount, unit, bound = work
             achieved = amount / avg_s
-            peak = FP32_MFMA_PEAK_TFLOPS if bound == "mfma" else HBM_PEAK_GBPS
+            peak = mfma_peak(dominant) if bound == "mfma" else HBM_PEAK_GBPS
             roof = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                    "frac": round(achieved / peak, 4), "traffic": load_traffic(dominant),
+                    "frac": round(achieved / peak, 4), "traffic": load_traffic(dominant) if headline else None,
                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt}
         # every phase with an algorithmic work model, from the untimed per-phase profiling steps
         per_kernel = {}
@@ -207,17 +243,17 @@ def main():
                 continue
             amt, unit, bnd = wk
             ach = amt / (pms / pcnt / 1e3)
-            pk = FP32_MFMA_PEAK_TFLOPS if bnd == "mfma" else HBM_PEAK_GBPS
+            pk = mfma_peak(ph) if bnd == "mfma" else HBM_PEAK_GBPS
             per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "frac": round(ach / pk, 4),
-                              "ms": round(pms / pcnt, 4), "traffic": load_traffic(ph)}
-        if roof is not None and dominant == "stft_mel":
+                              "ms": round(pms / pcnt, 4), "traffic": load_traffic(ph) if headline else None}
+        if roof is not None and dominant == "stft_mel" and args.attack == "ultrasonic":
             # the STFT moves few bytes per FLOP: its real limit is VALU issue (FFT butterflies),
             # reported beside the HBM fraction the metric asks for
             roof["note"] = ("HBM-bound by the survey's byte model but VALU-limited in practice: "
                             f"{stft_flops(args.batch, T) / avg_s / 1e12:.1f} TFLOP/s of FFT arithmetic "
                             f"(fp32 vector peak {FP32_MFMA_PEAK_TFLOPS})")
         cpu = None
-        if world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        if world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.attack == "ultrasonic":
             threads = min(16, len(os.sched_getaffinity(0)))
             cpu = cpu_baseline(args.cpu_sample, threads)
         line = {
@@ -231,12 +267,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.gemm_precision == "f32" else "bf16 conv GEMMs (fp32 accumulate), fp32 elsewhere",
             "data": "synthetic",
-            "config": {"workload": "ultrasonic.py (BASELINE configs[1]): 44.1 kHz x 1 s clips resident in HBM, "
-                                   "trigger add + HIP STFT (n_fft 1103 Bluestein)/mel/dB/DCT -> (1,100,40) + "
-                                   "smallcnn fp32 train step (fwd/bwd/CE/Adam) + ASR/acc counters",
-                       "attack": "ultrasonic", "num_classes": K, "per_gpu_batch": args.batch,
+            "config": {"workload": WORKLOADS[args.attack], "attack": args.attack, "num_classes": K,
+                       "gemm_precision": args.gemm_precision, "per_gpu_batch": args.batch,
                        "global_batch": args.batch * world, "poisoning_rate": cfg.poisoning_rate,
                        "resident_clips_per_gpu": args.n_train, "parallelism": f"dp{world}"},
             "roofline": roof,
