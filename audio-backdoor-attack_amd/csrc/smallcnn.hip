@@ -1087,13 +1087,20 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int NB, int EPI, int KB>
+// NP = 3 (ABD_PREC_F32_SPLIT): each fp32 operand x is staged as three bf16 planes x0 + x1 + x2 == x
+// exactly (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1: 8 + 8 + 8 significand bits), and the
+// product is accumulated from the six terms with i + j <= 2 (a2*b0, a0*b2, a1*b1, a1*b0, a0*b1,
+// a0*b0, small first).  Each term is exact in fp32 (8 x 8 bits); the dropped a1*b2 + a2*b1 + a2*b2
+// are <= ~2^-26 of |a*b|, below the 2^-24 rounding of one fp32 fma, so the GEMM carries fp32
+// accuracy at 6 x 32 MFMA cycles per 16-deep k-step instead of 8 x 64 for v_mfma_f32_32x32x2_f32.
+template <int NB, int EPI, int KB, int NP = 1>
 __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
+  static_assert(NP == 1 || NP == 3, "1 (bf16) or 3 (exact fp32 split) planes");
   constexpr int BM = kBM, LD = KB + 8, Q = KB / 4;  // Q float4 per row
   constexpr int RPT = BM * Q / kT, BPT = NB * Q / kT, NJ = NB / 32;
   static_assert(RPT >= 1 && BPT >= 1 && (BM * Q) % kT == 0 && (NB * Q) % kT == 0, "tile / thread mismatch");
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 As[NP][BM * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][NB * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * NB;
   const int q = tid % Q, r0 = tid / Q;
@@ -1130,13 +1137,19 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto cvt4 = [](float4 v) {
-    bf16x4 r;
-    r[0] = (__bf16)v.x;
-    r[1] = (__bf16)v.y;
-    r[2] = (__bf16)v.z;
-    r[3] = (__bf16)v.w;
-    return r;
+  // stage one float4 as NP bf16x4 planes, pstride elements apart
+  auto put = [](__bf16* p0, int pstride, float4 v) {
+    float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r[e] = (__bf16)x[e];
+        if (pl + 1 < NP) x[e] -= (float)r[e];  // exact: x - rne(x) fits in fp32
+      }
+      *reinterpret_cast<bf16x4*>(p0 + pl * pstride) = r;
+    }
   };
   f32x16 acc[NJ];
 #pragma unroll
@@ -1146,20 +1159,31 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   load(0);
   for (int ch = 0; ch < nch; ++ch) {
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) *reinterpret_cast<bf16x4*>(As + (r0 + RSTEP * i) * LD + 4 * q) = cvt4(ra[i]);
+    for (int i = 0; i < RPT; ++i) put(&As[0][(r0 + RSTEP * i) * LD + 4 * q], BM * LD, ra[i]);
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) *reinterpret_cast<bf16x4*>(Bs + (r0 + RSTEP * j) * LD + 4 * q) = cvt4(rbv[j]);
+    for (int j = 0; j < BPT; ++j) put(&Bs[0][(r0 + RSTEP * j) * LD + 4 * q], NB * LD, rbv[j]);
     __syncthreads();
     if (ch + 1 < nch) load(ch + 1);
-    const __bf16* ap = As + (wave * 32 + (lane & 31)) * LD + 8 * (lane >> 5);
-    const __bf16* bp = Bs + (lane & 31) * LD + 8 * (lane >> 5);
+    const int aoff = (wave * 32 + (lane & 31)) * LD + 8 * (lane >> 5);
+    const int boff = (lane & 31) * LD + 8 * (lane >> 5);
 #pragma unroll
     for (int ks = 0; ks < KB; ks += 16) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(ap + ks);
+      bf16x8 av[NP];
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) av[pl] = *reinterpret_cast<const bf16x8*>(&As[pl][aoff + ks]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp + j * 32 * LD + ks);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[j], 0, 0, 0);
+        bf16x8 bv[NP];
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) bv[pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl][boff + j * 32 * LD + ks]);
+        if constexpr (NP == 3) {
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc[j], 0, 0, 0);
+        }
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[j], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -1876,12 +1900,12 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 
-template <int NB, int EPI, int KB>
+template <int NB, int EPI, int KB, int NP = 1>
 int launch_nt_bf16(const NTArgs& a, hipStream_t s, int phase) {
   if (a.Cs % KB != 0 || a.ksplit > 1) return -1;
   dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB, 1);
   if (phase >= 0) abd::prof_begin(phase, s);
-  gemm_nt_bf16_kernel<NB, EPI, KB><<<grid, dim3(kT), 0, s>>>(a);
+  gemm_nt_bf16_kernel<NB, EPI, KB, NP><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -1989,11 +2013,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
-    const bool bf = net->precision == ABD_PREC_BF16;
-    a.nblk = bf ? (a.M + kBM - 1) / kBM : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
+    const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
+    a.nblk = (bf || sp) ? (a.M + kBM - 1) / kBM : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
+           : sp ? launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD)
            : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD)
            : kc64 ? launch_nt<64, EPI_CONV, 1, 64>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
@@ -2019,10 +2044,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   // ---- layer 3
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
-    const bool bf3 = net->precision == ABD_PREC_BF16;
-    a.nblk = bf3 ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
+    const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
+    a.nblk = (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (bf3 ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD) : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
+    if (bf3   ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD)
+        : sp3 ? launch_nt_bf16<32, EPI_CONV, 32, 3>(a, s, abd::PH_CONV3_FWD)
+              : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
       return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
@@ -2189,8 +2216,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                               kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s);
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
-    if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
-                                         : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
+    if (net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
+        : net->precision == ABD_PREC_F32_SPLIT ? launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD)
+                                               : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
       return -1;
   }
   // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
@@ -2221,6 +2249,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
+        : net->precision == ABD_PREC_F32_SPLIT ? launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD)
         : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
         : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
                                     : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
@@ -2299,7 +2328,7 @@ void abd_smallcnn_destroy(abd_cnn* net) { delete net; }
 
 int abd_smallcnn_set_precision(abd_cnn* net, int precision) {
   ABD_CHECK(net != nullptr, ABD_E_INVALID, "NULL net");
-  ABD_CHECK(precision == ABD_PREC_F32 || precision == ABD_PREC_BF16, ABD_E_INVALID, "unknown precision %d", precision);
+  ABD_CHECK(precision == ABD_PREC_F32 || precision == ABD_PREC_BF16 || precision == ABD_PREC_F32_SPLIT, ABD_E_INVALID, "unknown precision %d", precision);
   net->precision = precision;
   return ABD_OK;
 }

@@ -73,7 +73,7 @@ class _Engine:
         return self._ws
 
     def apply_precision(self, precision: str):
-        L.check(L.lib().abd_smallcnn_set_precision(self.h, L.PREC_BF16 if precision == "bf16" else L.PREC_F32),
+        L.check(L.lib().abd_smallcnn_set_precision(self.h, L.PRECISIONS[precision]),
                 "abd_smallcnn_set_precision")
 
     def views(self, buf):
@@ -124,10 +124,12 @@ class smallcnn(nn.Module):
 
     # ------------------------------------------------------------------ binding
     def set_gemm_precision(self, precision: str):
-        """'f32' (default, the reference's numerics) or 'bf16' (conv2/conv3 forward and data-gradient
-        GEMMs on v_mfma_f32_32x32x16_bf16, fp32 accumulation; BASELINE configs[2])."""
-        if precision not in ("f32", "bf16"):
-            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+        """'f32' (default, the reference's numerics: v_mfma_f32_32x32x2_f32), 'f32split' (the same
+        fp32-accurate products as exact three-way bf16 splits, six v_mfma_f32_32x32x16_bf16 terms)
+        or 'bf16' (operands rounded to bf16, fp32 accumulation; BASELINE configs[2]); applies to the
+        conv2/conv3 forward and data-gradient GEMMs."""
+        if precision not in L.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(L.PRECISIONS)}, got {precision!r}")
         self.gemm_precision = precision
         if self._engine is not None:
             self._engine.apply_precision(precision)

@@ -25,7 +25,8 @@ sys.path.insert(0, HERE)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec; 155 measured)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense ~2.5 PF (no sparsity)
-BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad")  # smallcnn GEMMs the bf16 mode moves
+BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad")  # smallcnn GEMMs the bf16 modes move
+SPLIT_TERMS = 6                 # f32split: six bf16 MFMA terms per fp32-accurate product
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -86,7 +87,11 @@ WORKLOADS = {
 def mfma_peak(phase, precision=None):
     """Dense MFMA peak of the dtype a phase's GEMM runs in (bf16 mode moves the conv fwd/dgrad GEMMs)."""
     prec = precision or _PRECISION[0]
-    return BF16_MFMA_PEAK_TFLOPS if (prec == "bf16" and phase in BF16_PHASES) else FP32_MFMA_PEAK_TFLOPS
+    if phase in BF16_PHASES and prec == "bf16":
+        return BF16_MFMA_PEAK_TFLOPS
+    if phase in BF16_PHASES and prec == "f32split":   # fp32 FLOPs at the bf16 rate / six terms
+        return BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS
+    return FP32_MFMA_PEAK_TFLOPS
 
 
 _PRECISION = ["f32"]
@@ -145,8 +150,9 @@ def main():
     ap.add_argument("--overlap", action="store_true", help="prefetch the next batch's features on a side stream")
     ap.add_argument("--attack", default="ultrasonic", help="workload: ultrasonic (headline, configs[1]), badnets, "
                     "jingleback, daba, flowmur")
-    ap.add_argument("--gemm-precision", default="f32", choices=("f32", "bf16"),
-                    help="conv GEMM precision (f32: the reference's numerics; bf16: BASELINE configs[2])")
+    ap.add_argument("--gemm-precision", default="f32", choices=("f32", "f32split", "bf16"),
+                    help="conv GEMM precision (f32: fp32 MFMA, the reference's numerics; f32split: the same "
+                         "fp32-accurate products as exact 3-way bf16 splits on bf16 MFMA; bf16: BASELINE configs[2])")
     args = ap.parse_args()
     _PRECISION[0] = args.gemm_precision
 
@@ -173,7 +179,7 @@ def main():
 
     abd_amd.load_library()
     cfg = attack_config(args.attack)
-    headline = args.attack == "ultrasonic" and args.gemm_precision == "f32"
+    headline = args.attack == "ultrasonic" and args.gemm_precision in ("f32", "f32split")
     K = 35 if args.attack == "ultrasonic" else 10
     waves, labels = synth.make_clips_torch(args.n_train, cfg.sample_rate, cfg.length, K, seed=35 + rank, device=dev)
     if cfg.clean_label:  # FlowMur poisons target-class clips only: make sure there are some
@@ -267,7 +273,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.gemm_precision == "f32" else "bf16 conv GEMMs (fp32 accumulate), fp32 elsewhere",
+            "dtype": {"f32": "f32", "f32split": "f32 (conv GEMMs as exact 3-way bf16 splits, 6 MFMA terms, fp32 accumulate)"}.get(
+                args.gemm_precision, "bf16 conv GEMMs (fp32 accumulate), fp32 elsewhere"),
             "data": "synthetic",
             "config": {"workload": WORKLOADS[args.attack], "attack": args.attack, "num_classes": K,
                        "gemm_precision": args.gemm_precision, "per_gpu_batch": args.batch,

@@ -216,8 +216,11 @@ int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn*
 /* GEMM precision of the conv2/conv3 forward and data-gradient products (BASELINE configs[2]:
  * "bf16, conv-as-GEMM on MFMA").  ABD_PREC_F32 (default): exact fp32 MFMA, the reference's
  * numerics.  ABD_PREC_BF16: operands rounded to bf16, fp32 accumulation (v_mfma_f32_32x32x16_bf16);
- * weight gradients, BatchNorm, fc layers and the loss stay fp32. */
-enum { ABD_PREC_F32 = 0, ABD_PREC_BF16 = 1 };
+ * weight gradients, BatchNorm, fc layers and the loss stay fp32.  ABD_PREC_F32_SPLIT: fp32
+ * operands split exactly into three bf16 planes (x = x0 + x1 + x2) and multiplied as the six
+ * terms with i + j <= 2 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- every term exact,
+ * dropped terms <= ~2^-26 |a*b| (below one fp32 rounding), i.e. fp32-accurate GEMMs. */
+enum { ABD_PREC_F32 = 0, ABD_PREC_BF16 = 1, ABD_PREC_F32_SPLIT = 2 };
 int abd_smallcnn_set_precision(abd_cnn* net, int precision);
 void abd_smallcnn_destroy(abd_cnn* net);
 int64_t abd_smallcnn_param_count(const abd_cnn* net);

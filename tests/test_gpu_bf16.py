@@ -1,4 +1,5 @@
-"""GPU: the opt-in bf16 conv GEMMs (abd_smallcnn_set_precision / smallcnn.set_gemm_precision).
+"""GPU: the bf16-MFMA conv GEMMs (abd_smallcnn_set_precision / smallcnn.set_gemm_precision):
+opt-in 'bf16' and the fp32-accurate 'f32split' (three exact bf16 planes per operand, six terms).
 
 Kernel exactness: each bf16 GEMM output the device wrote (conv2/conv3 forward -> r2/r3,
 conv3/conv2 data gradients -> dp2/dp1) equals the float64 product of the SAME device inputs
@@ -47,14 +48,18 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "f32split"])
 @pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 40)])
-def test_bf16_gemms_exact_on_rounded_operands(dev, shape):
+def test_bf16_gemms_exact_on_rounded_operands(dev, shape, prec):
+    """bf16: exact products of the bf16-rounded operands.  f32split: the six-term exact bf16
+    split of the UNROUNDED fp32 operands -- the same 2e-6 bound as against the float64 product."""
     H, W, K, B = shape
+    rnd = bf16 if prec == "bf16" else (lambda a: np.asarray(a, np.float64))
     g = oc.geometry(H, W)
     st = make_state(H, W, K, g["flat"], seed=77 + H)
     m = M.smallcnn(K, g["flat"])
     m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
-    m = m.to(dev).train().set_gemm_precision("bf16")
+    m = m.to(dev).train().set_gemm_precision(prec)
     r = np.random.Generator(np.random.PCG64(H + B))
     x = torch.tensor(mfcc_like(r, B, H, W), device=dev)
     y = torch.tensor(r.integers(0, K, B), device=dev)
@@ -70,12 +75,12 @@ def test_bf16_gemms_exact_on_rounded_operands(dev, shape):
     dp2 = ws_view(eng, ws, B, "dp2", (B, g["H2p"], g["W2p"], 64))
     dz2 = ws_view(eng, ws, B, "dz2", (B, g["H2"], g["W2"], 64))
     dp1 = ws_view(eng, ws, B, "dp1", (B, g["H1p"], g["W1p"], 64))
-    w2 = bf16(st["conv2.weight"])
-    w3 = bf16(st["conv3.weight"])
-    ref_r2 = np.maximum(oc.conv2x2(bf16(nchw(p1)), w2, st["conv2.bias"].astype(np.float64)), 0.0)
-    ref_r3 = np.maximum(oc.conv2x2(bf16(nchw(p2)), w3, st["conv3.bias"].astype(np.float64)), 0.0)
-    ref_dp2, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H2p"], g["W2p"])), w3, bf16(nchw(dz3)))
-    ref_dp1, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H1p"], g["W1p"])), w2, bf16(nchw(dz2)))
+    w2 = rnd(st["conv2.weight"])
+    w3 = rnd(st["conv3.weight"])
+    ref_r2 = np.maximum(oc.conv2x2(rnd(nchw(p1)), w2, st["conv2.bias"].astype(np.float64)), 0.0)
+    ref_r3 = np.maximum(oc.conv2x2(rnd(nchw(p2)), w3, st["conv3.bias"].astype(np.float64)), 0.0)
+    ref_dp2, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H2p"], g["W2p"])), w3, rnd(nchw(dz3)))
+    ref_dp1, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H1p"], g["W1p"])), w2, rnd(nchw(dz2)))
     errs = {"r2": nrel(nchw(r2), ref_r2), "r3": nrel(nchw(r3), ref_r3), "dp2": nrel(nchw(dp2), ref_dp2),
             "dp1": nrel(nchw(dp1), ref_dp1)}
     print(shape, {k: f"{v:.1e}" for k, v in errs.items()})
@@ -84,7 +89,10 @@ def test_bf16_gemms_exact_on_rounded_operands(dev, shape):
     # and the products really are bf16: the exact-fp32 product differs by ~bf16 rounding
     ref32 = np.maximum(oc.conv2x2(nchw(p1), st["conv2.weight"].astype(np.float64),
                                   st["conv2.bias"].astype(np.float64)), 0.0)
-    assert nrel(nchw(r2), ref32) > 1e-4
+    if prec == "bf16":
+        assert nrel(nchw(r2), ref32) > 1e-4
+    else:
+        assert nrel(nchw(r2), ref32) < 2e-6
 
 
 def test_bf16_logprobs_close_to_fp32(dev):

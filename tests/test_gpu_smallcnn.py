@@ -1,4 +1,7 @@
-"""GPU parity: libabd smallcnn (fp32 MFMA) vs the reference's golden outputs and the float64 oracle."""
+"""GPU parity: libabd smallcnn vs the reference's golden outputs and the float64 oracle.
+
+Every parity test runs for both fp32-accurate GEMM modes: 'f32' (v_mfma_f32_32x32x2_f32) and
+'f32split' (exact three-way bf16 splits, six v_mfma_f32_32x32x16_bf16 terms) at the same tolerance."""
 import numpy as np
 import pytest
 import torch
@@ -30,10 +33,13 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def build(st, K, lf, dev):
+PRECS = ("f32", "f32split")
+
+
+def build(st, K, lf, dev, prec="f32"):
     m = M.smallcnn(K, lf)
     m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
-    return m.to(dev)
+    return m.to(dev).set_gemm_precision(prec)
 
 
 def nrel(a, b):
@@ -42,23 +48,25 @@ def nrel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", list(EVAL_CFGS))
-def test_eval_matches_reference_golden(dev, golden, name):
+def test_eval_matches_reference_golden(dev, golden, name, prec):
     H, W, K, lf = EVAL_CFGS[name]
     st = make_state(H, W, K, lf, seed=1000 + H * 7 + W + K, trained_bn=True)
-    m = build(st, K, lf, dev).eval()
+    m = build(st, K, lf, dev, prec).eval()
     with torch.no_grad():
         y = m(torch.tensor(eval_inputs(H, W), device=dev)).cpu().numpy()
     ref = golden[f"eval_{name}_logprobs"]
     np.testing.assert_allclose(y, ref, rtol=RTOL, atol=RTOL * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", list(TRAIN_CFGS))
-def test_train_epoch_matches_reference_golden(dev, golden, name):
+def test_train_epoch_matches_reference_golden(dev, golden, name, prec):
     """Reference train() + test() (utils/training_tools.py) with its dropout masks injected."""
     H, W, K, lf, B, NB = TRAIN_CFGS[name]
     st = make_state(H, W, K, lf, seed=2000 + H * 7 + W + K, trained_bn=False)
-    m = build(st, K, lf, dev).train()
+    m = build(st, K, lf, dev, prec).train()
     opt = torch.optim.Adam(m.parameters(), lr=1e-4)
     x, y, ind, xc, yc, xb, yb, ib = train_inputs(H, W, K, B, NB)
     flat = oc.geometry(H, W)["flat"]
@@ -99,14 +107,15 @@ def test_train_epoch_matches_reference_golden(dev, golden, name):
     assert te[2] == pytest.approx(ref_te[2], rel=RTOL) and te[3] == pytest.approx(ref_te[3], rel=RTOL)
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("shape", [(101, 40, 10, 64), (100, 40, 35, 96), (32, 40, 10, 64), (32, 13, 10, 48)])
-def test_train_step_gradients_vs_oracle(dev, shape):
+def test_train_step_gradients_vs_oracle(dev, shape, prec):
     """Large-batch step: device-generated dropout masks fed to the float64 oracle; grads/params/stats compared."""
     H, W, K, B = shape
     g = oc.geometry(H, W)
     lf = g["flat"]
     st = make_state(H, W, K, lf, seed=3000 + H + W + K)
-    m = build(st, K, lf, dev).train()
+    m = build(st, K, lf, dev, prec).train()
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     r = np.random.Generator(np.random.PCG64(H * W + B))
     x = mfcc_like(r, B, H, W)
