@@ -170,7 +170,13 @@ struct C1Args {
 __device__ __forceinline__ void stage_x(const C1Args& a, int b, int h0, float* xs) {
   const int rows = min(a.rows + 1, a.g.H0 - h0);
   const float* src = a.x + ((int64_t)b * a.g.H0 + h0) * a.g.W0;
-  for (int i = threadIdx.x; i < rows * a.g.W0; i += kT) xs[i] = src[i];
+  if ((a.g.W0 & 3) == 0) {  // rows start 16-byte aligned: one float4 per thread (W0 = 40: 90 loads)
+    const int n4 = rows * a.g.W0 / 4;
+    for (int i = threadIdx.x; i < n4; i += kT)
+      reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(src)[i];
+  } else {
+    for (int i = threadIdx.x; i < rows * a.g.W0; i += kT) xs[i] = src[i];
+  }
   __syncthreads();
 }
 
@@ -223,7 +229,7 @@ __device__ __forceinline__ float4 c1_coef_col(const float4* coef, int c0, int co
 
 // forward stats: sum / sumsq of relu(conv1) per channel
 __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
-  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
@@ -268,7 +274,7 @@ __device__ __forceinline__ int c1_argmax(float r0, float r1, float r2, float al,
 
 // forward: relu(conv1) -> BN1 -> maxpool(1,3) -> p1 (NHWC)
 __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
-  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
@@ -301,7 +307,7 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
 
 // backward stats: s1 = sum dy, s2 = sum dy * xhat over pool1 argmax positions
 __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
-  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
@@ -340,8 +346,10 @@ __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
 
 // backward: BN1 dx -> relu mask -> conv1 weight / bias gradient partials (5 per channel).
 // 2 channels per thread (the double-precision BN coefficients would otherwise cap occupancy).
+// FULL (W1 % 3 == 0, every BASELINE geometry): no partial trailing window, branch-free body.
+template <bool FULL>
 __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
-  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
   constexpr int CPT = 2;
@@ -367,8 +375,8 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     for (int idx = pl; idx < rows * NW; idx += kT / 32) {
       const int hl = idx / NW, wo = idx - hl * NW;
       const int w = 3 * wo;
-      const int nw = min(3, a.g.W1 - w);
-      const bool real = wo < a.g.W1p;
+      const int nw = FULL ? 3 : min(3, a.g.W1 - w);
+      const bool real = FULL || wo < a.g.W1p;
       const float* x0 = xs + hl * a.g.W0 + w;
       float xv[2][4];
   #pragma unroll
@@ -551,7 +559,7 @@ __device__ __forceinline__ float4 bn_coef_from_sums(double s, double ss, double 
 // relu(conv1) statistics of utterance blockIdx.x (recomputed from x like conv1_stats_kernel)
 __global__ void __launch_bounds__(kT) inst_conv1_coef_kernel(C1Args a, const float* gamma, const float* beta,
                                                              float4* coef) {
-  __shared__ float xs[(kR1 + 1) * 128];
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   __shared__ double red[2][16][64];
   const int b = blockIdx.x;
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
@@ -1426,6 +1434,101 @@ __global__ void __launch_bounds__(kT, 4) conv_wgrad_rows_kernel(WGArgs a) {
 }
 
 // sum slabs in order; conv layout maps (n=co, k=t*Cin+ci) -> torch (co, ci, kh, kw)
+// Exact three-way bf16 split of 8 fp32 values (x = p0 + p1 + p2, see gemm_nt_bf16_kernel).
+__device__ __forceinline__ void split3_x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)x[e];
+    const float r1 = x[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    p0[e] = h;
+    p1[e] = m;
+    p2[e] = (__bf16)(r1 - (float)m);
+  }
+}
+
+// conv_wgrad_rows_kernel with fp32-accurate products on bf16 MFMA (opt-in: ABD_WGRAD_SPLIT=1 with
+// ABD_PREC_F32_SPLIT; measured 0.21-0.26 ms vs 0.18 ms for the fp32 kernel at B = 512, 100x40 --
+// the strided scalar LDS reads and in-register splits cost more than the MFMA cycles saved): the same
+// row chunks staged by global_load_lds into the same LDS images; the reduction over positions
+// m' runs 16 at a time (v_mfma_f32_32x32x16_bf16: lane half h holds m' = mb + 8h .. +7), each
+// operand split in registers into three exact bf16 planes, six terms per tile.  Positions past
+// the chunk's rows * Ws are masked to zero in the dz operand (their source reads land in the
+// zeroed slack or in finite stale data).
+template <int NB, int CIN>
+__global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_wg[];
+  constexpr int KT = 4 * CIN / 32, TILES = (NB / 32) * KT, TPW = TILES / 4;
+  static_assert(TILES % 4 == 0 && KT % TPW == 0, "a wave's tiles must share one n-tile");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, col = lane & 31;
+  const int nt = (wave * TPW) / KT;
+  const int rowd = a.Wo * NB / 4;
+  int boff[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int kt = (wave * TPW + i) % KT;
+    const int tap = kt / (CIN / 32), cb = kt % (CIN / 32);
+    boff[i] = ((tap >> 1) * a.Ws + (tap & 1)) * CIN + cb * 32 + col;
+  }
+  for (int i = threadIdx.x; i < 2 * a.bsz; i += kT) lds_wg[i] = 0.0f;
+  __syncthreads();
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
+  auto stage = [&](int c, float* buf) {
+    const int b = c / a.cpb, h0 = (c - b * a.cpb) * a.R;
+    const int rows = min(a.R, a.Ho - h0);
+    const float* g = a.dz + ((int64_t)b * a.Ho + h0) * a.Wo * NB;
+    for (int r = 0; r < rows; ++r) glds_copy(g + r * a.Wo * NB, buf + r * a.Ws * NB, rowd);
+    glds_copy(a.src + ((int64_t)b * a.Hs + h0) * a.Ws * CIN, buf + a.dsz, (rows + 1) * a.Ws * CIN / 4);
+  };
+  if (c0 < c1) stage(c0, lds_wg);
+  for (int c = c0; c < c1; ++c) {
+    float* cur = lds_wg + ((c - c0) & 1) * a.bsz;
+    __syncthreads();
+    if (c + 1 < c1) stage(c + 1, lds_wg + ((c + 1 - c0) & 1) * a.bsz);
+    const int h0 = (c % a.cpb) * a.R;
+    const int mlim = min(a.R, a.Ho - h0) * a.Ws;
+    const float* D = cur + nt * 32 + col;
+    const float* S = cur + a.dsz;
+    for (int mb = 0; mb < mlim; mb += 16) {
+      const int m0 = mb + 8 * half;
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = (m0 + e < mlim) ? D[(m0 + e) * NB] : 0.0f;
+      bf16x8 a0, a1, a2;
+      split3_x8(x, a0, a1, a2);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = S[(m0 + e) * CIN + boff[i]];
+        bf16x8 b0, b1, b2;
+        split3_x8(x, b0, b1, b2);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[i], 0, 0, 0);
+      }
+    }
+  }
+  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int k = ((wave * TPW + i) % KT) * 32 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      slab[(int64_t)n * (4 * CIN) + k] = acc[i][r];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int nslab, int N, int Ktot, int conv_cin,
                                                          float* out) {
   const int64_t total = (int64_t)N * Ktot;
@@ -1858,7 +1961,7 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 // resident block count (occupancy API) capped by the slab buffer.
 template <int NB, int CIN>
 int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int R,
-                      int max_slabs, float* slab, int phase, hipStream_t s) {
+                      int max_slabs, float* slab, int phase, hipStream_t s, bool split = false) {
   ABD_CHECK(Ws == Wo + 1 && Hs >= Ho + 1, ABD_E_UNSUPPORTED, "wgrad geometry");
   WGArgs a{};
   a.dz = dz;
@@ -1872,14 +1975,17 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
   a.nchunks = (int)(B * a.cpb);
   // dz on the Ws-strided grid; source rows + one slack row (a pad position's dh = 1 tap
   // reads one row past the chunk)
-  a.dsz = ((a.R * Ws + 2) * NB + 3) & ~3;  // + 2 positions for the one-ahead read
-  a.bsz = (a.dsz + (a.R + 2) * Ws * CIN + 3) & ~3;
+  // split: 16-position groups read up to 15 positions past the chunk (masked dz; source slack)
+  const int slackp = split ? 16 : 2;
+  a.dsz = ((a.R * Ws + slackp) * NB + 3) & ~3;  // + positions for the one-ahead / group read
+  a.bsz = (a.dsz + ((a.R + 2) * Ws + (split ? 16 : 0)) * CIN + 3) & ~3;
   a.slab = slab;
   const size_t lds = 2 * (size_t)a.bsz * sizeof(float);
-  auto* kern = &conv_wgrad_rows_kernel<NB, CIN>;
-  static size_t cached_lds = 0;
-  static int per_cu = 1, n_cu = 256;
-  if (cached_lds != lds) {
+  auto* kern = split ? &conv_wgrad_rows_split_kernel<NB, CIN> : &conv_wgrad_rows_kernel<NB, CIN>;
+  static size_t cached_lds[2] = {0, 0};
+  static int per_cu_c[2] = {1, 1}, n_cu = 256;
+  int& per_cu = per_cu_c[split];
+  if (cached_lds[split] != lds) {
     ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
     int dev = 0;
@@ -1887,7 +1993,7 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
     ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kT, lds));
     per_cu = std::max(1, per_cu);
-    cached_lds = lds;
+    cached_lds[split] = lds;
   }
   int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
   a.per = (a.nchunks + grid - 1) / grid;
@@ -2212,8 +2318,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, G[P_C3B]);
     ABD_LAUNCH_CHECK();
+    const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
-                                              kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s);
+                                              kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s, spw);
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if (net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
@@ -2243,8 +2350,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     partial_sum_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, G[P_C2B]);
     ABD_LAUNCH_CHECK();
-    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, env_int("ABD_WGRAD_R2", 1),
-                                              kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s);
+    const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
+    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
+                                              spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
+                                              kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s, spw);
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
@@ -2275,7 +2384,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     ABD_LAUNCH_CHECK();
     c1.bcoef = w.bcoef;
     abd::prof_begin(abd::PH_CONV1_BWD, s);
-    conv1_wgrad_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    if (g.W1 % 3 == 0)
+      conv1_wgrad_kernel<true><<<c1.nblk, kT, 0, s>>>(c1);
+    else
+      conv1_wgrad_kernel<false><<<c1.nblk, kT, 0, s>>>(c1);
     abd::prof_end(abd::PH_CONV1_BWD, s);
     ABD_LAUNCH_CHECK();
     // part rows: j*64 + c, j = 0..3 weights (kh,kw), 4 bias -> conv1.w is (c,1,kh,kw): transpose via tiny pass
