@@ -1094,6 +1094,8 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
 // groups); wave w owns rows 32w..32w+31 x all NB columns (NB / 32 accumulators).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // NP = 3 (ABD_PREC_F32_SPLIT): each fp32 operand x is staged as three bf16 planes x0 + x1 + x2 == x
 // exactly (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1: 8 + 8 + 8 significand bits), and the
@@ -1101,10 +1103,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // a0*b0, small first).  Each term is exact in fp32 (8 x 8 bits); the dropped a1*b2 + a2*b1 + a2*b2
 // are <= ~2^-26 of |a*b|, below the 2^-24 rounding of one fp32 fma, so the GEMM carries fp32
 // accuracy at 6 x 32 MFMA cycles per 16-deep k-step instead of 8 x 64 for v_mfma_f32_32x32x2_f32.
-template <int NB, int EPI, int KB, int NP = 1>
+// MI = 32-row m-tiles per wave (block rows 128 * MI): MI = 2 halves the LDS reads per MFMA
+// (2 A + 2 B fragments per plane feed 4 accumulators), which the 3-plane split is bound by.
+template <int NB, int EPI, int KB, int NP = 1, int MI = 1>
 __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   static_assert(NP == 1 || NP == 3, "1 (bf16) or 3 (exact fp32 split) planes");
-  constexpr int BM = kBM, LD = KB + 8, Q = KB / 4;  // Q float4 per row
+  constexpr int BM = kBM * MI, LD = KB + 8, Q = KB / 4;  // Q float4 per row
   constexpr int RPT = BM * Q / kT, BPT = NB * Q / kT, NJ = NB / 32;
   static_assert(RPT >= 1 && BPT >= 1 && (BM * Q) % kT == 0 && (NB * Q) % kT == 0, "tile / thread mismatch");
   __shared__ __attribute__((aligned(16))) __bf16 As[NP][BM * LD];
@@ -1113,17 +1117,41 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * NB;
   const int q = tid % Q, r0 = tid / Q;
   constexpr int RSTEP = kT / Q;
-  int rb[RPT], rh[RPT], rw[RPT];
-  bool rok[RPT];
+  // Operands through buffer loads: A's descriptor starts at the block's first image, so each row
+  // is a 32-bit byte offset; a tap outside the source grid (or a row past M) loads from kOOB, which
+  // the descriptor's range check turns into zeros.  Per chunk: one add + one select per row.
+  constexpr uint32_t kOOB = 0x80000000u;
+  const int HoWo = a.Ho * a.Wo;
+  const int b0 = m0 / HoWo;
+  const int64_t img = (int64_t)a.Hs * a.Ws * a.Cs;
+  const int64_t abytes = (int64_t)((a.M + HoWo - 1) / HoWo - b0) * img * 4;
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.src + b0 * img), 0, (int)(abytes < 0x7ffffff0 ? abytes : 0x7ffffff0), 0x00020000);
+  const int64_t bbytes = (int64_t)a.N * a.ldb * 4;
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.Bw), 0, (int)(bbytes < 0x7ffffff0 ? bbytes : 0x7ffffff0), 0x00020000);
+  uint32_t roff[RPT], tmask[RPT], boff[BPT];
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int m = m0 + r0 + RSTEP * i;
-    rok[i] = m < a.M;
-    const int mm = rok[i] ? m : 0;
-    rb[i] = mm / (a.Ho * a.Wo);
-    const int rem = mm - rb[i] * a.Ho * a.Wo;
-    rh[i] = rem / a.Wo;
-    rw[i] = rem - rh[i] * a.Wo;
+    const bool rok = m < a.M;
+    const int mm = rok ? m : m0;
+    const int rb = mm / HoWo;
+    const int rem = mm - rb * HoWo;
+    const int rh = rem / a.Wo, rw = rem - rh * a.Wo;
+    roff[i] = (uint32_t)(((((int64_t)(rb - b0) * a.Hs + rh) * a.Ws + rw) * a.Cs + 4 * q) * 4);
+    uint32_t mk = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int hs = rh + a.dh[t], ws = rw + a.dw[t];
+      if (t < a.taps && rok && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
+    }
+    tmask[i] = mk;
+  }
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int n = n0 + r0 + RSTEP * j;
+    boff[j] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + 4 * q) * 4) : kOOB;
   }
   const int cpt = a.Cs / KB;
   const int nch = a.taps * cpt;
@@ -1131,39 +1159,43 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   auto load = [&](int ch) {
     const int t = ch / cpt;
     const int c0 = (ch - t * cpt) * KB;
+    const uint32_t adelta = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * a.Cs + c0) * 4);
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const int hs = rh[i] + a.dh[t], ws = rw[i] + a.dw[t];
-      const bool ok = rok[i] && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws;
-      ra[i] = ok ? *reinterpret_cast<const float4*>(a.src + (((int64_t)rb[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c0 + 4 * q)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      const uint32_t off = (tmask[i] >> t) & 1u ? roff[i] + adelta : kOOB;
+      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
     }
+    const uint32_t bdelta = (uint32_t)((t * a.Cs + c0) * 4);
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) {
-      const int n = r0 + RSTEP * j;
-      rbv[j] = (n0 + n < a.N) ? *reinterpret_cast<const float4*>(a.Bw + (int64_t)(n0 + n) * a.ldb + t * a.Cs + c0 + 4 * q)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < BPT; ++j)
+      rbv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)(boff[j] + bdelta), 0, 0));
   };
-  // stage one float4 as NP bf16x4 planes, pstride elements apart
+  // stage one float4 as NP bf16x4 planes, pstride elements apart.  Pairs: one v_cvt_pk_bf16_f32
+  // (RNE), the two bf16 widened back by bit moves, one v_pk_add_f32 for the exact residual.
   auto put = [](__bf16* p0, int pstride, float4 v) {
-    float x[4] = {v.x, v.y, v.z, v.w};
+    f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
 #pragma unroll
     for (int pl = 0; pl < NP; ++pl) {
-      bf16x4 r;
+      uint32_t u[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        r[e] = (__bf16)x[e];
-        if (pl + 1 < NP) x[e] -= (float)r[e];  // exact: x - rne(x) fits in fp32
+      for (int h = 0; h < 2; ++h) {
+        const bf16x2 r = __builtin_convertvector(x[h], bf16x2);
+        u[h] = __builtin_bit_cast(uint32_t, r);
+        if (pl + 1 < NP) {
+          const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+          x[h] -= back;  // exact: x - rne(x) fits in fp32
+        }
       }
-      *reinterpret_cast<bf16x4*>(p0 + pl * pstride) = r;
+      *reinterpret_cast<uint2*>(p0 + pl * pstride) = make_uint2(u[0], u[1]);
     }
   };
-  f32x16 acc[NJ];
+  f32x16 acc[MI][NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   load(0);
   for (int ch = 0; ch < nch; ++ch) {
 #pragma unroll
@@ -1172,26 +1204,31 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
     for (int j = 0; j < BPT; ++j) put(&Bs[0][(r0 + RSTEP * j) * LD + 4 * q], NB * LD, rbv[j]);
     __syncthreads();
     if (ch + 1 < nch) load(ch + 1);
-    const int aoff = (wave * 32 + (lane & 31)) * LD + 8 * (lane >> 5);
+    const int aoff = (wave * 32 * MI + (lane & 31)) * LD + 8 * (lane >> 5);
     const int boff = (lane & 31) * LD + 8 * (lane >> 5);
 #pragma unroll
     for (int ks = 0; ks < KB; ks += 16) {
-      bf16x8 av[NP];
+      bf16x8 av[MI][NP];
 #pragma unroll
-      for (int pl = 0; pl < NP; ++pl) av[pl] = *reinterpret_cast<const bf16x8*>(&As[pl][aoff + ks]);
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) av[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl][aoff + i * 32 * LD + ks]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         bf16x8 bv[NP];
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl) bv[pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl][boff + j * 32 * LD + ks]);
-        if constexpr (NP == 3) {
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          if constexpr (NP == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bv[0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bv[1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bv[0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[1], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[0], acc[i][j], 0, 0, 0);
         }
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[j], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -1206,10 +1243,12 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
     float bias = 0.0f;
     if constexpr (EPI == EPI_CONV) bias = cok ? a.bias[col] : 0.0f;
 #pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int m = m0 + wave * 32 * MI + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= a.M || !cok) continue;
-      float v = acc[j][r];
+      float v = acc[i][j][r];
       if constexpr (EPI == EPI_CONV) {
         v = fmaxf(v + bias, 0.0f);
         st[j][0] += v;
@@ -2006,12 +2045,19 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 
-template <int NB, int EPI, int KB, int NP = 1>
+// rows per wave (x32) of the 3-plane conv2 GEMMs; ABD_SPLIT_MI=1 restores the 128-row tiles
+static int split_mi() {
+  static const int mi = env_int("ABD_SPLIT_MI", 1) == 1 ? 1 : 2;
+  return mi;
+}
+
+template <int NB, int EPI, int KB, int NP = 1, int MI = 1>
 int launch_nt_bf16(const NTArgs& a, hipStream_t s, int phase) {
   if (a.Cs % KB != 0 || a.ksplit > 1) return -1;
-  dim3 grid((a.M + kBM - 1) / kBM, (a.N + NB - 1) / NB, 1);
+  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != (a.M + kBM * MI - 1) / (kBM * MI)) return -1;
+  dim3 grid((a.M + kBM * MI - 1) / (kBM * MI), (a.N + NB - 1) / NB, 1);
   if (phase >= 0) abd::prof_begin(phase, s);
-  gemm_nt_bf16_kernel<NB, EPI, KB, NP><<<grid, dim3(kT), 0, s>>>(a);
+  gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -2120,11 +2166,14 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
-    a.nblk = (bf || sp) ? (a.M + kBM - 1) / kBM : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
+    a.nblk = bf ? (a.M + kBM - 1) / kBM
+             : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
+             : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
-           : sp ? launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD)
+           : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
+                                   : launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD))
            : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD)
            : kc64 ? launch_nt<64, EPI_CONV, 1, 64>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
@@ -2358,7 +2407,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
-        : net->precision == ABD_PREC_F32_SPLIT ? launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD)
+        : net->precision == ABD_PREC_F32_SPLIT
+            ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
+                               : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD))
         : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
         : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
                                     : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
