@@ -780,6 +780,24 @@ __device__ __forceinline__ int pooled_index(const PoolArgs& a, int b, int ho, in
   return ((b * a.Ho + ho) * a.Wo + wo) * a.C + c;
 }
 
+// the 4 channels' pooled gradients of one window: one float4 load in the NHWC layout (pool2),
+// 4 strided loads in the NCHW-flat layout feeding fc1 (pool3)
+__device__ __forceinline__ void load_dy4(const PoolArgs& a, int b, int ho, int wo, int c0, bool real, float (&dy)[4]) {
+  if (!real) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dy[q] = 0.0f;
+  } else if (a.flat_n == 0) {
+    const float4 d = *reinterpret_cast<const float4*>(a.dp + pooled_index(a, b, ho, wo, c0));
+    dy[0] = d.x;
+    dy[1] = d.y;
+    dy[2] = d.z;
+    dy[3] = d.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dy[q] = a.dp[pooled_index(a, b, ho, wo, c0 + q)];
+  }
+}
+
 __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
   const int CG = a.C / 4;
   const int total = a.B * a.Ho * a.Wo * CG;
@@ -826,9 +844,11 @@ __global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) {
     float best[4];
     int arg[4];
     win_argmax(a, wi.b, wi.ho, wi.wo, c0, cf, rv, in, best, arg);
+    float dyv[4];
+    load_dy4(a, wi.b, wi.ho, wi.wo, c0, true, dyv);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float dy = a.dp[pooled_index(a, wi.b, wi.ho, wi.wo, c0 + q)];
+      const float dy = dyv[q];
       float r = 0.0f;
 #pragma unroll
       for (int slot = 0; slot < 4; ++slot) r = (arg[q] == slot) ? f4get(rv[slot], q) : r;
@@ -862,8 +882,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a, int Hx, in
     int arg[4];
     win_argmax(a, wi.b, wi.ho, wi.wo, c0, cf, rv, in, best, arg);
     float dy[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dy[q] = real ? a.dp[pooled_index(a, wi.b, wi.ho, wi.wo, c0 + q)] : 0.0f;
+    load_dy4(a, wi.b, wi.ho, wi.wo, c0, real, dy);
 #pragma unroll
     for (int slot = 0; slot < 4; ++slot) {
       if (!in[slot]) continue;
@@ -2266,6 +2285,12 @@ int launch_conv_halo_split(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
+// K-chunk depth of the 3-plane conv2 GEMMs (ABD_SPLIT_KB=16: 28 KB of LDS per block, 4 waves/SIMD)
+static int split_kb() {
+  static const int kb = env_int("ABD_SPLIT_KB", 32) == 16 ? 16 : 32;
+  return kb;
+}
+
 // rows per wave (x32) of the 3-plane conv2 GEMMs; ABD_SPLIT_MI=1 restores the 128-row tiles
 static int split_mi() {
   static const int mi = env_int("ABD_SPLIT_MI", 1) == 1 ? 1 : 2;
@@ -2396,7 +2421,8 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
            : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
                    : launch_conv_halo_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD) == 0
                        ? 0
-                       : launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD))
+                   : split_kb() == 16 ? launch_nt_bf16<64, EPI_CONV, 16, 3>(a, s, abd::PH_CONV2_FWD)
+                                      : launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD))
            : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD)
            : kc64 ? launch_nt<64, EPI_CONV, 1, 64>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
@@ -2634,7 +2660,8 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
             ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
                : launch_conv_halo_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0
                    ? 0
-                   : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD))
+               : split_kb() == 16 ? launch_nt_bf16<64, EPI_STORE, 16, 3>(da, s, abd::PH_CONV2_DGRAD)
+                                  : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD))
         : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
         : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
                                     : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
