@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--fp32-mode", default="f32split", choices=("f32split", "f32"),
+                    help="conv GEMMs of the fp32 configs (f32split = bench.py's default, fp32-accurate)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -48,13 +50,14 @@ def main():
         print(json.dumps(d), flush=True)
 
     # ---- training step per attack (BASELINE configs[0..4] at one GPU)
-    plan = [("badnets", 10, 256, "f32", "configs[0] badnets.py (GPU form of the CPU-only reference config)"),
-            ("ultrasonic", 35, 512, "f32", "configs[1] ultrasonic.py (headline; bench.py)"),
+    FP = args.fp32_mode
+    plan = [("badnets", 10, 256, FP, "configs[0] badnets.py (GPU form of the CPU-only reference config)"),
+            ("ultrasonic", 35, 512, FP, "configs[1] ultrasonic.py (headline; bench.py)"),
             ("ultrasonic", 35, 512, "bf16", "configs[1] shape with bf16 conv GEMMs (not the headline: fp32 parity)"),
-            ("jingleback", 10, 256, "f32", "configs[2] jingleback.py style 5, fp32 GEMMs"),
+            ("jingleback", 10, 256, FP, "configs[2] jingleback.py style 5, fp32-accurate GEMMs"),
             ("jingleback", 10, 256, "bf16", "configs[2] jingleback.py style 5, bf16 conv GEMMs on MFMA (the config's dtype)"),
-            ("daba", 10, 256, "f32", "configs[3] daba.py training step (librosa 32x40 features)"),
-            ("flowmur", 10, 256, "f32", "configs[4] flowmur.py poisoned training (smallcnn 32x13)")]
+            ("daba", 10, 256, FP, "configs[3] daba.py training step (librosa 32x40 features)"),
+            ("flowmur", 10, 256, FP, "configs[4] flowmur.py poisoned training (smallcnn 32x13)")]
     for name, K, B, prec, what in plan:
         if only and name not in only:
             continue
