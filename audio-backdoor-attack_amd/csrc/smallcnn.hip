@@ -681,6 +681,22 @@ __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, 
 
 // sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
 // conv1 mode (gw != nullptr): columns j*64 + c, j < 4 -> conv1.weight (c,1,kh,kw) = gw[c*4 + j], j = 4 -> gb[c]
+// sum_{i < n} p[i * stride] in index order (the same rounding as a serial loop), loads issued
+// 8 at a time so a thread keeps 8 HBM reads in flight
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ p, int64_t stride, int n) {
+  float v = 0.0f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = p[(int64_t)(i + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += t[j];
+  }
+  for (; i < n; ++i) v += p[(int64_t)i * stride];
+  return v;
+}
+
 __global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out,
                                                          float* gw = nullptr, float* gb = nullptr) {
   const int col = blockIdx.x;
@@ -1781,8 +1797,7 @@ __global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int 
                                                          float* out) {
   const int64_t total = (int64_t)N * Ktot;
   for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    float s = 0.0f;
-    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * total + e];
+    const float s = ordered_sum(slab + e, total, nslab);
     const int n = (int)(e / Ktot), k = (int)(e % Ktot);
     if (conv_cin > 0) {
       const int t = k / conv_cin, ci = k % conv_cin;
@@ -1930,8 +1945,7 @@ __global__ void __launch_bounds__(kT) fc1_epilogue_kernel(const float* part, int
                                                           DropArgs drop, float* d2) {
   const int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x;
   if (e >= (int64_t)B * 128) return;
-  float v = 0.0f;
-  for (int z = 0; z < ks; ++z) v += part[(int64_t)z * B * 128 + e];
+  const float v = ordered_sum(part + e, (int64_t)B * 128, ks);
   d2[e] = drop_apply(drop, e, fmaxf(v + bias[e & 127], 0.0f));
 }
 
@@ -1969,9 +1983,7 @@ __global__ void __launch_bounds__(kT) slab_group_kernel(const float* slab, int n
   if (e >= total) return;
   const int g = blockIdx.y;
   const int i0 = g * gsize, i1 = min(nslab, i0 + gsize);
-  float s = 0.0f;
-  for (int i = i0; i < i1; ++i) s += slab[(int64_t)i * total + e];
-  part[(int64_t)g * total + e] = s;
+  part[(int64_t)g * total + e] = ordered_sum(slab + (int64_t)i0 * total + e, total, i1 - i0);
 }
 
 // column sums of a (rows, cols) matrix: one block per column, fixed reduction tree
