@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(kThreads) db_dct_kernel(MfccDev p, const float
 
 // db_dct with the DCT matrix in LDS: block = (utterance, 16 frames); thread = (frame, 4
 // consecutive coefficients); the dB tile is read with broadcasts, the matrix row as float4.
-constexpr int kTT2 = 16;
+constexpr int kTT2 = 16;  // frames per db_dct_lds block (52 measured equal: 0.039 ms at B = 512, 100 frames)
 __global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const float* __restrict__ ws_db,
                                                               const float* __restrict__ ws_max, InjDev inj,
                                                               float* __restrict__ out) {
@@ -461,26 +461,28 @@ __global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const f
   for (int i = threadIdx.x; i < nt * p.n_mels; i += kThreads) db[i] = fmaxf(src[i], floor_db);
   __syncthreads();
   const int cg4 = p.n_mfcc / 4;
-  const int t = threadIdx.x / cg4, c0 = (threadIdx.x - t * cg4) * 4;
-  if (t >= nt) return;
-  const float* d = db + t * p.n_mels;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int m = 0; m < p.n_mels; ++m) {
-    const float x = d[m];
-    const float4 w = *reinterpret_cast<const float4*>(dct + m * p.n_mfcc + c0);
-    acc.x = fmaf(x, w.x, acc.x);
-    acc.y = fmaf(x, w.y, acc.y);
-    acc.z = fmaf(x, w.z, acc.z);
-    acc.w = fmaf(x, w.w, acc.w);
+  const bool pois = inj.patch && row_poisoned(inj, u);
+  for (int o = threadIdx.x; o < nt * cg4; o += kThreads) {
+    const int t = o / cg4, c0 = (o - t * cg4) * 4;
+    const float* d = db + t * p.n_mels;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < p.n_mels; ++m) {
+      const float x = d[m];
+      const float4 w = *reinterpret_cast<const float4*>(dct + m * p.n_mfcc + c0);
+      acc.x = fmaf(x, w.x, acc.x);
+      acc.y = fmaf(x, w.y, acc.y);
+      acc.z = fmaf(x, w.z, acc.z);
+      acc.w = fmaf(x, w.w, acc.w);
+    }
+    const int tt = t0 + t;
+    if (pois && tt >= inj.pt0 && tt < inj.pt1) {
+      float* a = &acc.x;
+      for (int q = 0; q < 4; ++q)
+        if (c0 + q >= inj.pc0 && c0 + q < inj.pc1) a[q] = inj.pval;
+    }
+    if (tt >= nv) acc = make_float4(inj.fpad, inj.fpad, inj.fpad, inj.fpad);
+    *reinterpret_cast<float4*>(out + ((int64_t)u * p.T + tt) * p.n_mfcc + c0) = acc;
   }
-  const int tt = t0 + t;
-  if (inj.patch && row_poisoned(inj, u) && tt >= inj.pt0 && tt < inj.pt1) {
-    float* a = &acc.x;
-    for (int q = 0; q < 4; ++q)
-      if (c0 + q >= inj.pc0 && c0 + q < inj.pc1) a[q] = inj.pval;
-  }
-  if (tt >= nv) acc = make_float4(inj.fpad, inj.fpad, inj.fpad, inj.fpad);
-  *reinterpret_cast<float4*>(out + ((int64_t)u * p.T + tt) * p.n_mfcc + c0) = acc;
 }
 
 __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __restrict__ wave, int64_t row_stride,
@@ -1887,7 +1889,7 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   ABD_LAUNCH_CHECK();
   abd::prof_begin(abd::PH_DB_DCT, s);
   const size_t dct_lds = ((size_t)d.n_mels * d.n_mfcc + (size_t)kTT2 * d.n_mels) * sizeof(float);
-  if (d.n_mfcc % 4 == 0 && kTT2 * (d.n_mfcc / 4) <= kThreads && dct_lds <= 64 * 1024 &&
+  if (d.n_mfcc % 4 == 0 && dct_lds <= 64 * 1024 &&
       (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
       getenv("ABD_DCT_GENERIC") == nullptr) {
     db_dct_lds_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT2 - 1) / kTT2)), dim3(kThreads), dct_lds, s>>>(
