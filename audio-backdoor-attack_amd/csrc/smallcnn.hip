@@ -206,15 +206,25 @@ __device__ __forceinline__ C1W c1_weights(const C1Args& a, int c0) {
 }
 
 // relu(conv1) at (hl, w) for 4 channels; same fma order as the oracle replay (b, w00, w01, w10, w11)
-__device__ __forceinline__ float4 c1_at(const float* xs, int W0, int hl, int w, const C1W& k) {
-  const float* r0 = xs + hl * W0 + w;
+// relu(conv1) for 4 channels at one position: channel pairs on v_pk_fma_f32, the same fma chain
+// per channel as the oracle replay (b, w00, w01, w10, w11)
+typedef float c1f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ c1f2 c1_lo(const float4& v) { return c1f2{v.x, v.y}; }
+__device__ __forceinline__ c1f2 c1_hi(const float4& v) { return c1f2{v.z, v.w}; }
+__device__ __forceinline__ float4 c1_at_ptr(const float* r0, int W0, const C1W& k) {
   const float x00 = r0[0], x01 = r0[1], x10 = r0[W0], x11 = r0[W0 + 1];
-  float4 v;
-  v.x = fmaxf(fmaf(k.w11.x, x11, fmaf(k.w10.x, x10, fmaf(k.w01.x, x01, fmaf(k.w00.x, x00, k.b.x)))), 0.0f);
-  v.y = fmaxf(fmaf(k.w11.y, x11, fmaf(k.w10.y, x10, fmaf(k.w01.y, x01, fmaf(k.w00.y, x00, k.b.y)))), 0.0f);
-  v.z = fmaxf(fmaf(k.w11.z, x11, fmaf(k.w10.z, x10, fmaf(k.w01.z, x01, fmaf(k.w00.z, x00, k.b.z)))), 0.0f);
-  v.w = fmaxf(fmaf(k.w11.w, x11, fmaf(k.w10.w, x10, fmaf(k.w01.w, x01, fmaf(k.w00.w, x00, k.b.w)))), 0.0f);
-  return v;
+  c1f2 lo = __builtin_elementwise_fma(c1_lo(k.w00), c1f2{x00, x00}, c1_lo(k.b));
+  c1f2 hi = __builtin_elementwise_fma(c1_hi(k.w00), c1f2{x00, x00}, c1_hi(k.b));
+  lo = __builtin_elementwise_fma(c1_lo(k.w01), c1f2{x01, x01}, lo);
+  hi = __builtin_elementwise_fma(c1_hi(k.w01), c1f2{x01, x01}, hi);
+  lo = __builtin_elementwise_fma(c1_lo(k.w10), c1f2{x10, x10}, lo);
+  hi = __builtin_elementwise_fma(c1_hi(k.w10), c1f2{x10, x10}, hi);
+  lo = __builtin_elementwise_fma(c1_lo(k.w11), c1f2{x11, x11}, lo);
+  hi = __builtin_elementwise_fma(c1_hi(k.w11), c1f2{x11, x11}, hi);
+  return make_float4(fmaxf(lo.x, 0.0f), fmaxf(lo.y, 0.0f), fmaxf(hi.x, 0.0f), fmaxf(hi.y, 0.0f));
+}
+__device__ __forceinline__ float4 c1_at(const float* xs, int W0, int hl, int w, const C1W& k) {
+  return c1_at_ptr(xs + hl * W0 + w, W0, k);
 }
 
 __device__ __forceinline__ float4 c1_coef_col(const float4* coef, int c0, int comp) {
@@ -239,9 +249,15 @@ __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
+    // positions pl, pl + 16, ... in row-major (hl, w) order, stepped without dividing by W1
+    int hl = pl / a.g.W1, w = pl - hl * a.g.W1;
     for (int idx = pl; idx < rows * a.g.W1; idx += 16) {
-      const int hl = idx / a.g.W1, w = idx - hl * a.g.W1;
       const float4 r = c1_at(xs, a.g.W0, hl, w, k);
+      w += 16;
+      while (w >= a.g.W1) {
+        w -= a.g.W1;
+        ++hl;
+      }
       v[0][0] += r.x;
       v[0][1] += r.y;
       v[0][2] += r.z;
@@ -289,8 +305,12 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
     }
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
-    for (int idx = pl; idx < rows * NW; idx += 16) {
-      const int hl = idx / NW, wo = idx - hl * NW;
+    int hl = pl / NW, wo = pl - hl * NW;  // (hl, wo) of idx, stepped without dividing by NW
+    for (int idx = pl; idx < rows * NW; idx += 16, wo += 16) {
+      while (wo >= NW) {
+        wo -= NW;
+        ++hl;
+      }
       const int w = 3 * wo;
       const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
                    r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
@@ -320,8 +340,12 @@ __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
-    for (int idx = pl; idx < rows * NW; idx += 16) {
-      const int hl = idx / NW, wo = idx - hl * NW;
+    int hl = pl / NW, wo = pl - hl * NW;  // (hl, wo) of idx, stepped without dividing by NW
+    for (int idx = pl; idx < rows * NW; idx += 16, wo += 16) {
+      while (wo >= NW) {
+        wo -= NW;
+        ++hl;
+      }
       const int w = 3 * wo;
       const float4 r0 = c1_at(xs, a.g.W0, hl, w, k), r1 = c1_at(xs, a.g.W0, hl, w + 1, k),
                    r2 = c1_at(xs, a.g.W0, hl, w + 2, k);
@@ -367,13 +391,23 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     bc[q] = a.bcoef[c0 + q];
   }
   const int NW = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
-  float v[5][CPT] = {};
+  static_assert(CPT == 2, "one packed channel pair per thread");
+  c1f2 kp[5], vp[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    kp[t] = c1f2{kw[0][t], kw[1][t]};
+    vp[t] = c1f2{0.0f, 0.0f};
+  }
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
-    for (int idx = pl; idx < rows * NW; idx += kT / 32) {
-      const int hl = idx / NW, wo = idx - hl * NW;
+    int hl = pl / NW, wo = pl - hl * NW;  // (hl, wo) of idx, stepped without dividing by NW
+    for (int idx = pl; idx < rows * NW; idx += kT / 32, wo += kT / 32) {
+      while (wo >= NW) {
+        wo -= NW;
+        ++hl;
+      }
       const int w = 3 * wo;
       const int nw = FULL ? 3 : min(3, a.g.W1 - w);
       const bool real = FULL || wo < a.g.W1p;
@@ -392,30 +426,44 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
       } else {
         dd[0] = dd[1] = 0.0f;
       }
+      // the channel pair on v_pk_fma_f32: per channel the same fma chain as the oracle replay
+      // (b, w00, w01, w10, w11) and the same accumulation order
+      float r[CPT][3];
+  #pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        c1f2 acc = __builtin_elementwise_fma(kp[0], c1f2{xv[0][j], xv[0][j]}, kp[4]);
+        acc = __builtin_elementwise_fma(kp[1], c1f2{xv[0][j + 1], xv[0][j + 1]}, acc);
+        acc = __builtin_elementwise_fma(kp[2], c1f2{xv[1][j], xv[1][j]}, acc);
+        acc = __builtin_elementwise_fma(kp[3], c1f2{xv[1][j + 1], xv[1][j + 1]}, acc);
+        r[0][j] = (j < nw) ? fmaxf(acc.x, 0.0f) : 0.0f;
+        r[1][j] = (j < nw) ? fmaxf(acc.y, 0.0f) : 0.0f;
+      }
+      int jm[CPT];
   #pragma unroll
       for (int q = 0; q < CPT; ++q) {
-        float r[3];
-  #pragma unroll
-        for (int j = 0; j < 3; ++j)  // same fma order as the oracle replay (b, w00, w01, w10, w11)
-          r[j] = (j < nw) ? fmaxf(fmaf(kw[q][3], xv[1][j + 1], fmaf(kw[q][2], xv[1][j], fmaf(kw[q][1], xv[0][j + 1],
-                                                                                            fmaf(kw[q][0], xv[0][j], kw[q][4])))),
-                                  0.0f)
-                          : 0.0f;
         float best;
-        const int jm = real ? c1_argmax(r[0], r[1], r[2], aa[q], bb[q], best) : -1;
+        jm[q] = real ? c1_argmax(r[q][0], r[q][1], r[q][2], aa[q], bb[q], best) : -1;
+      }
   #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (j >= nw) continue;
-          const float dz = r[j] > 0.0f ? bn_dx(j == jm ? dd[q] : 0.0f, r[j], float4{}, bc[q]) : 0.0f;
-          v[0][q] = fmaf(dz, xv[0][j], v[0][q]);
-          v[1][q] = fmaf(dz, xv[0][j + 1], v[1][q]);
-          v[2][q] = fmaf(dz, xv[1][j], v[2][q]);
-          v[3][q] = fmaf(dz, xv[1][j + 1], v[3][q]);
-          v[4][q] += dz;
-        }
+      for (int j = 0; j < 3; ++j) {
+        if (j >= nw) continue;
+        c1f2 dz;
+        dz.x = r[0][j] > 0.0f ? bn_dx(j == jm[0] ? dd[0] : 0.0f, r[0][j], float4{}, bc[0]) : 0.0f;
+        dz.y = r[1][j] > 0.0f ? bn_dx(j == jm[1] ? dd[1] : 0.0f, r[1][j], float4{}, bc[1]) : 0.0f;
+        vp[0] = __builtin_elementwise_fma(dz, c1f2{xv[0][j], xv[0][j]}, vp[0]);
+        vp[1] = __builtin_elementwise_fma(dz, c1f2{xv[0][j + 1], xv[0][j + 1]}, vp[1]);
+        vp[2] = __builtin_elementwise_fma(dz, c1f2{xv[1][j], xv[1][j]}, vp[2]);
+        vp[3] = __builtin_elementwise_fma(dz, c1f2{xv[1][j + 1], xv[1][j + 1]}, vp[3]);
+        vp[4] += dz;
       }
     }
     __syncthreads();  // xs is restaged by the next chunk
+  }
+  float v[5][CPT];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    v[t][0] = vp[t].x;
+    v[t][1] = vp[t].y;
   }
   cgroup_partials<5, CPT>(v, 64, a.part, a.nblk, blockIdx.x);
 }
