@@ -2648,10 +2648,16 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     a.ldc = g.flat;
     a.drop = drop1;
     a.drop.mask_in = drop1.enabled ? w.mask1 : nullptr;
+    // 32-column tiles: M = B rows is short (4 row tiles at B = 512), so 128-column tiles leave
+    // most CUs idle (96 blocks); ABD_FC1D_NB=128 restores them
+    static const bool nb128 = env_int("ABD_FC1D_NB", 32) == 128;
     if (drop1.enabled) {
-      if (launch_nt<128, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD)) return -1;
+      if (nb128 ? launch_nt<128, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD)
+                : launch_nt<32, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD))
+        return -1;
     } else {
-      if (launch_nt<128, EPI_STORE>(a, s, abd::PH_FC1_DGRAD)) return -1;
+      if (nb128 ? launch_nt<128, EPI_STORE>(a, s, abd::PH_FC1_DGRAD) : launch_nt<32, EPI_STORE>(a, s, abd::PH_FC1_DGRAD))
+        return -1;
     }
   }
   // ---- pool3 / BN3 / relu backward -> dz3; conv3 wgrad + dgrad
