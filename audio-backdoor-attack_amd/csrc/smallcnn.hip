@@ -1977,15 +1977,19 @@ __global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B
 }
 
 // fc2 data gradient through dropout2/ReLU: da = (dz . W2) * scale2 * [d2 > 0]
-__global__ void __launch_bounds__(kT) fc2_bwd_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
-                                                     float scale2, float* da) {
+__device__ __forceinline__ void fc2_bwd_body(const float* dz, const float* d2, const float* w2, int B, int K,
+                                             float scale2, float* da, int bx, int nb) {
   const int64_t nd = (int64_t)B * 128;
-  for (int64_t f = blockIdx.x * (int64_t)kT + threadIdx.x; f < nd; f += (int64_t)gridDim.x * kT) {
+  for (int64_t f = bx * (int64_t)kT + threadIdx.x; f < nd; f += (int64_t)nb * kT) {
     const int b = (int)(f / 128), j = (int)(f % 128);
     float s = 0.0f;
     for (int k = 0; k < K; ++k) s = fmaf(dz[(int64_t)b * K + k], w2[(int64_t)k * 128 + j], s);
     da[f] = d2[f] > 0.0f ? s * scale2 : 0.0f;
   }
+}
+__global__ void __launch_bounds__(kT) fc2_bwd_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
+                                                     float scale2, float* da) {
+  fc2_bwd_body(dz, d2, w2, B, K, scale2, da, blockIdx.x, gridDim.x);
 }
 
 // fc1: sum the split-K partials in order, + bias, ReLU, dropout2 -> d2
@@ -1998,9 +2002,8 @@ __global__ void __launch_bounds__(kT) fc1_epilogue_kernel(const float* part, int
 }
 
 // fc2 weight/bias gradient partials: grid (K, nsplit); 128 threads = hidden units
-__global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const float* d2, int B, int K, int rows,
-                                                       float* part) {
-  const int k = blockIdx.x, sp = blockIdx.y, j = threadIdx.x;
+__device__ __forceinline__ void fc2_wgrad_body(const float* dz, const float* d2, int B, int K, int rows, float* part,
+                                               int k, int sp, int j) {
   const int b0 = sp * rows, b1 = min(B, b0 + rows);
   float s = 0.0f, sb = 0.0f;
 #pragma unroll 4
@@ -2012,16 +2015,35 @@ __global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const f
   part[((int64_t)sp * K + k) * 129 + j] = s;
   if (j == 0) part[((int64_t)sp * K + k) * 129 + 128] = sb;
 }
+__global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const float* d2, int B, int K, int rows,
+                                                       float* part) {
+  fc2_wgrad_body(dz, d2, B, K, rows, part, blockIdx.x, blockIdx.y, threadIdx.x);
+}
 
-__global__ void __launch_bounds__(kT) fc2_wgrad_reduce_kernel(const float* part, int nsplit, int K, float* gw,
-                                                              float* gb) {
-  const int e = blockIdx.x * kT + threadIdx.x;
+// fc2_wgrad_kernel and fc2_bwd_kernel in one launch (independent: both only read dz and d2):
+// blocks [0, nw) run two 128-thread (k, split) groups each, the rest fc2_bwd's grid-stride loop
+__global__ void __launch_bounds__(kT) fc2_grads_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
+                                                       int rows, int nsplit, float* part, float scale2, float* da,
+                                                       int nw) {
+  if ((int)blockIdx.x < nw) {
+    const int pr = (int)blockIdx.x * 2 + (int)(threadIdx.x >> 7);
+    if (pr < K * nsplit) fc2_wgrad_body(dz, d2, B, K, rows, part, pr % K, pr / K, threadIdx.x & 127);
+    return;
+  }
+  fc2_bwd_body(dz, d2, w2, B, K, scale2, da, (int)blockIdx.x - nw, (int)gridDim.x - nw);
+}
+
+__device__ __forceinline__ void fc2_wgrad_reduce_body(const float* part, int nsplit, int K, float* gw, float* gb, int e) {
   if (e >= K * 129) return;
   float s = 0.0f;
   for (int i = 0; i < nsplit; ++i) s += part[(int64_t)i * K * 129 + e];
   const int k = e / 129, j = e % 129;
   if (j < 128) gw[k * 128 + j] = s;
   else gb[k] = s;
+}
+__global__ void __launch_bounds__(kT) fc2_wgrad_reduce_kernel(const float* part, int nsplit, int K, float* gw,
+                                                              float* gb) {
+  fc2_wgrad_reduce_body(part, nsplit, K, gw, gb, blockIdx.x * kT + threadIdx.x);
 }
 
 // stage 1 of the slab reduction: group sums (each group = up to 32 slabs, in order)
@@ -2035,8 +2057,7 @@ __global__ void __launch_bounds__(kT) slab_group_kernel(const float* slab, int n
 }
 
 // column sums of a (rows, cols) matrix: one block per column, fixed reduction tree
-__global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, int cols, float* out) {
-  const int c = blockIdx.x;
+__device__ __forceinline__ void colsum_body(const float* x, int rows, int cols, float* out, int c) {
   double s = 0.0;
   for (int r = threadIdx.x; r < rows; r += kT) s += x[(int64_t)r * cols + c];
   __shared__ double red[kT / kWave];
@@ -2044,6 +2065,20 @@ __global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, in
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+__global__ void __launch_bounds__(kT) colsum_kernel(const float* x, int rows, int cols, float* out) {
+  colsum_body(x, rows, cols, out, blockIdx.x);
+}
+// fc2_wgrad_reduce_kernel and colsum_kernel (fc1 bias gradient) in one launch: blocks [0, cols)
+// are the column sums, the rest the split reduction
+__global__ void __launch_bounds__(kT) fc2_reduce_colsum_kernel(const float* part, int nsplit, int K, float* gw,
+                                                               float* gb, const float* x, int rows, int cols,
+                                                               float* out) {
+  if ((int)blockIdx.x < cols) {
+    colsum_body(x, rows, cols, out, blockIdx.x);
+    return;
+  }
+  fc2_wgrad_reduce_body(part, nsplit, K, gw, gb, ((int)blockIdx.x - cols) * kT + threadIdx.x);
 }
 
 // ------------------------------------------------------------------ Adam (torch single-tensor semantics)
@@ -2597,11 +2632,12 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   abd::prof_begin(abd::PH_FC2_BWD, s);
   {
     const int rows = (int)((B + kFc2Split - 1) / kFc2Split);
-    fc2_wgrad_kernel<<<dim3((unsigned)g.K, (unsigned)kFc2Split), 128, 0, s>>>(w.dz, w.d2, (int)B, g.K, rows, w.slab2);
-    fc2_wgrad_reduce_kernel<<<(unsigned)((g.K * 129 + kT - 1) / kT), kT, 0, s>>>(w.slab2, kFc2Split, g.K, G[P_F2W],
-                                                                                G[P_F2B]);
-    fc2_bwd_kernel<<<grid_for(B * 128), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, s2, w.da);
-    colsum_kernel<<<128, kT, 0, s>>>(w.da, (int)B, 128, G[P_F1B]);
+    // two launches instead of four: [fc2 weight-grad partials | da] then [their reduction | fc1 bias]
+    const int nw = (g.K * kFc2Split + 1) / 2;
+    fc2_grads_kernel<<<(unsigned)(nw + grid_for(B * 128)), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, rows,
+                                                                       kFc2Split, w.slab2, s2, w.da, nw);
+    fc2_reduce_colsum_kernel<<<(unsigned)(128 + (g.K * 129 + kT - 1) / kT), kT, 0, s>>>(
+        w.slab2, kFc2Split, g.K, G[P_F2W], G[P_F2B], w.da, (int)B, 128, G[P_F1B]);
   }
   abd::prof_end(abd::PH_FC2_BWD, s);
   ABD_LAUNCH_CHECK();
