@@ -745,9 +745,8 @@ __device__ __forceinline__ float ordered_sum(const float* __restrict__ p, int64_
   return v;
 }
 
-__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out,
-                                                         float* gw = nullptr, float* gb = nullptr) {
-  const int col = blockIdx.x;
+__device__ __forceinline__ void partial_sum_body(const float* part, int nblk, float* out, float* gw, float* gb,
+                                                 int col) {
   double s = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) s += part[(int64_t)col * nblk + i];
   __shared__ double red[kT / kWave];
@@ -761,6 +760,17 @@ __global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int 
     else gb[col - 4 * 64] = v;
   }
 }
+__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* part, int nblk, int ncols, float* out,
+                                                         float* gw = nullptr, float* gb = nullptr) {
+  partial_sum_body(part, nblk, out, gw, gb, blockIdx.x);
+}
+
+// a conv bias gradient (column sums of BN-backward partials) carried by another launch
+struct BiasSum {
+  const float* part = nullptr;
+  int nblk = 0, ncols = 0;
+  float* out = nullptr;
+};
 
 // ------------------------------------------------------------------ BN + max-pool (layers 2, 3)
 struct PoolArgs {
@@ -2047,8 +2057,14 @@ __global__ void __launch_bounds__(kT) fc2_wgrad_reduce_kernel(const float* part,
 }
 
 // stage 1 of the slab reduction: group sums (each group = up to 32 slabs, in order)
+// bs.part != nullptr: the last grid row (blockIdx.y == gridDim.y - 1) instead computes the
+// independent bias-gradient column sums, one block per column
 __global__ void __launch_bounds__(kT) slab_group_kernel(const float* slab, int nslab, int64_t total, int gsize,
-                                                        float* part) {
+                                                        float* part, BiasSum bs) {
+  if (bs.part != nullptr && blockIdx.y == gridDim.y - 1) {
+    if ((int)blockIdx.x < bs.ncols) partial_sum_body(bs.part, bs.nblk, bs.out, nullptr, nullptr, blockIdx.x);
+    return;
+  }
   const int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x;
   if (e >= total) return;
   const int g = blockIdx.y;
@@ -2434,14 +2450,21 @@ int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
-int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s) {
+int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s,
+                 BiasSum bias = BiasSum{}) {
   const int64_t total = (int64_t)N * Ktot;
   const float* src = w.slab;
   int n = nsl;
+  const unsigned gx = (unsigned)((total + kT - 1) / kT);
+  const bool carry = bias.part != nullptr && nsl > kSlabGroup && (int64_t)gx >= bias.ncols;
+  if (bias.part != nullptr && !carry) {
+    partial_sum_kernel<<<(unsigned)bias.ncols, kT, 0, s>>>(bias.part, bias.nblk, bias.ncols, bias.out);
+    ABD_LAUNCH_CHECK();
+  }
   if (nsl > kSlabGroup) {
     const int G = (nsl + kSlabGroup - 1) / kSlabGroup;
-    slab_group_kernel<<<dim3((unsigned)((total + kT - 1) / kT), (unsigned)G), kT, 0, s>>>(w.slab, nsl, total,
-                                                                                         kSlabGroup, w.slab2);
+    slab_group_kernel<<<dim3(gx, (unsigned)(G + (carry ? 1 : 0))), kT, 0, s>>>(w.slab, nsl, total, kSlabGroup,
+                                                                                w.slab2, carry ? bias : BiasSum{});
     ABD_LAUNCH_CHECK();
     src = w.slab2;
     n = G;
@@ -2716,12 +2739,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
-    partial_sum_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, G[P_C3B]);
-    ABD_LAUNCH_CHECK();
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
                                               kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s, spw);
-    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s)) return -1;
+    // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
+    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.part, pa.nblk, 32, G[P_C3B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if (net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
         : net->precision == ABD_PREC_F32_SPLIT ? launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD)
@@ -2748,13 +2770,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
-    partial_sum_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, G[P_C2B]);
-    ABD_LAUNCH_CHECK();
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
                                               spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
                                               kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s, spw);
-    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s)) return -1;
+    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s, BiasSum{w.part, pa.nblk, 64, G[P_C2B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
