@@ -71,8 +71,14 @@ class TrainArgs(C.Structure):
         ("mask1_in", C.c_void_p), ("mask2_in", C.c_void_p), ("seed", C.c_uint64), ("counter", C.c_uint64),
         ("mask1_out", C.c_void_p), ("mask2_out", C.c_void_p), ("logprobs_out", C.c_void_p),
         ("metrics", C.c_void_p), ("grad_scale", C.c_float), ("num_batches_tracked", C.c_void_p),
-        ("fc_grads_event", C.c_void_p),
+        ("fc_grads_event", C.c_void_p), ("row_offset", C.c_int64),
+        ("bn_sync_buf", C.c_void_p), ("bn_sync", C.c_void_p), ("bn_sync_ctx", C.c_void_p),
     ]
+
+
+# int (*bn_sync)(void* ctx, int point, int64_t offset, int64_t n)  (abd_train_args.bn_sync)
+BN_SYNC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int64)
+BN_SYNC_STRIDE = 136
 
 
 class AbdError(RuntimeError):

@@ -84,13 +84,14 @@ struct DropArgs {
   const uint8_t* mask_in;
   uint8_t* mask_out;
   uint64_t seed, stream;
+  uint64_t base;  // global element index of this launch's element 0 (DP: row_offset * columns)
   float p, scale;
   int enabled;
 };
 
 __device__ __forceinline__ float drop_apply(const DropArgs& d, int64_t idx, float v) {
   if (!d.enabled) return v;
-  bool k = d.mask_in ? (d.mask_in[idx] != 0) : keep_hash(d.seed, d.stream, (uint64_t)idx, d.p);
+  bool k = d.mask_in ? (d.mask_in[idx] != 0) : keep_hash(d.seed, d.stream, d.base + (uint64_t)idx, d.p);
   if (d.mask_out) d.mask_out[idx] = k ? 1 : 0;
   return v * (k ? d.scale : 0.0f);
 }
@@ -725,6 +726,78 @@ __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, 
     const double mean = (double)coef[c].x, invstd = (double)coef[c].y;
     bcoef[c] = BCoef{g, g * (mdyx * invstd * mean - mdy), -g * mdyx * invstd, 0.0};
   }
+}
+
+// ------------------------------------------------------------------ synchronised BatchNorm
+// The SyncBN path splits each finalize in two around the caller's all-reduce: this rank's
+// double sums (the same fixed-tree reduction as the kernels above) -> SUM over ranks ->
+// coefficients from the global sums and count.  On one rank the result is bit-identical to
+// bn_finalize_kernel / bn_bwd_finalize_kernel.
+__device__ __forceinline__ void block_pair_sum(const float* part, int nblk, int C, int c, double& s, double& ss) {
+  s = 0.0;
+  ss = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kT) {
+    s += part[(int64_t)c * nblk + i];
+    ss += part[((int64_t)C + c) * nblk + i];
+  }
+  __shared__ double red[2][kT / kWave];
+  s = abd::wave_sum_d(s);
+  ss = abd::wave_sum_d(ss);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = ss;
+  }
+  __syncthreads();
+  s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  ss = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+}
+
+// out[c] = sum_c, out[C + c] = sum2_c, out[2C] = count; backward (dgamma != nullptr) also writes
+// this rank's BN weight / bias gradient shares
+__global__ void __launch_bounds__(kT) bn_local_sums_kernel(const float* part, int nblk, int C, double count,
+                                                           double* out, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x;
+  double s, ss;
+  block_pair_sum(part, nblk, C, c, s, ss);
+  if (threadIdx.x == 0) {
+    out[c] = s;
+    out[C + c] = ss;
+    if (c == 0) out[2 * C] = count;
+    if (dgamma) {
+      dgamma[c] = (float)ss;
+      dbeta[c] = (float)s;
+    }
+  }
+}
+
+__global__ void bn_sync_finalize_kernel(const double* sums, int C, const float* gamma, const float* beta, float* rm,
+                                        float* rv, float4* coef, int64_t* nbt) {
+  const int c = threadIdx.x;
+  if (nbt != nullptr && c < 3) nbt[c] += 1;
+  if (c >= C) return;
+  const double count = sums[2 * C];
+  const double mean = sums[c] / count;
+  double var = sums[C + c] / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)kEps));
+  const float alpha = gamma[c] * invstd;
+  const float meanf = (float)mean;
+  coef[c] = make_float4(meanf, invstd, alpha, beta[c] - meanf * alpha);
+  if (rm) {
+    const double mo = (double)kMomentum;
+    rm[c] = (float)(mo * mean + (1.0 - mo) * (double)rm[c]);
+    rv[c] = (float)(mo * (var * count / (count - 1.0)) + (1.0 - mo) * (double)rv[c]);
+  }
+}
+
+__global__ void bn_sync_bwd_finalize_kernel(const double* sums, int C, const float* gamma, const float4* coef,
+                                            BCoef* bcoef) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const double count = sums[2 * C], s1 = sums[c], s2 = sums[C + c];
+  const double g = (double)gamma[c] * (double)coef[c].y, mdy = s1 / count, mdyx = s2 / count;
+  const double mean = (double)coef[c].x, invstd = (double)coef[c].y;
+  bcoef[c] = BCoef{g, g * (mdyx * invstd * mean - mdy), -g * mdyx * invstd, 0.0};
 }
 
 // sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
@@ -2474,10 +2547,68 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
   return 0;
 }
 
+// -------------------------------------------------------------- synchronised BatchNorm (host)
+struct BnSync {
+  double* buf = nullptr;
+  int (*fn)(void*, int, int64_t, int64_t) = nullptr;
+  void* ctx = nullptr;
+  bool on() const { return buf != nullptr && fn != nullptr; }
+};
+
+BnSync bn_sync_of(const abd_train_args* a) {
+  BnSync y;
+  if (a && a->bn_sync_buf && a->bn_sync) {
+    y.buf = a->bn_sync_buf;
+    y.fn = a->bn_sync;
+    y.ctx = a->bn_sync_ctx;
+  }
+  return y;
+}
+
+// point 0..2: forward bn1..bn3; 3..5: backward bn3..bn1
+int sync_point(const BnSync& y, int point, int C) {
+  const int rc = y.fn(y.ctx, point, (int64_t)point * ABD_BN_SYNC_STRIDE, 2 * C + 1);
+  ABD_CHECK(rc == 0, ABD_E_INVALID, "bn_sync callback failed at point %d (%d)", point, rc);
+  return 0;
+}
+
+// train-mode BatchNorm statistics -> coefficients (+ running statistics), per rank or synchronised
+int bn_fwd_finalize(const BnSync& y, int point, const float* part, int nblk, int C, double count, const float* gamma,
+                    const float* beta, float* rm, float* rv, float4* coef, int64_t* nbt, hipStream_t s) {
+  if (!y.on()) {
+    bn_finalize_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, gamma, beta, rm, rv, coef, nbt);
+    ABD_LAUNCH_CHECK();
+    return 0;
+  }
+  double* buf = y.buf + (int64_t)point * ABD_BN_SYNC_STRIDE;
+  bn_local_sums_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, buf, nullptr, nullptr);
+  ABD_LAUNCH_CHECK();
+  if (sync_point(y, point, C)) return -1;
+  bn_sync_finalize_kernel<<<1, 64, 0, s>>>(buf, C, gamma, beta, rm, rv, coef, nbt);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
+int bn_bwd_finalize(const BnSync& y, int point, const float* part, int nblk, int C, double count, const float* gamma,
+                    const float4* coef, float* dgamma, float* dbeta, BCoef* bcoef, hipStream_t s) {
+  if (!y.on()) {
+    bn_bwd_finalize_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, gamma, coef, dgamma, dbeta, bcoef);
+    ABD_LAUNCH_CHECK();
+    return 0;
+  }
+  double* buf = y.buf + (int64_t)point * ABD_BN_SYNC_STRIDE;
+  bn_local_sums_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, buf, dgamma, dbeta);
+  ABD_LAUNCH_CHECK();
+  if (sync_point(y, point, C)) return -1;
+  bn_sync_bwd_finalize_kernel<<<1, 64, 0, s>>>(buf, C, gamma, coef, bcoef);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
-            int64_t* nbt = nullptr, float4* inst_coef = nullptr) {
+            int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{}) {
   // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
   // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
@@ -2515,8 +2646,9 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     conv1_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
     abd::prof_end(abd::PH_CONV1_STATS, s);
     ABD_LAUNCH_CHECK();
-    bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B],
-                                         rmu[0], rvu[0], w.coef, running_upd ? nbt : nullptr);
+    if (bn_fwd_finalize(sy, 0, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B], rmu[0],
+                        rvu[0], w.coef, running_upd ? nbt : nullptr, s))
+      return -1;
   } else {
     bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN1W], P.p[P_BN1B], rm[0], rv[0], 64, w.coef);
   }
@@ -2547,10 +2679,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
                                                   inst_coef + B * 64);
-    else if (train)
-      bn_finalize_kernel<<<64, kT, 0, s>>>(w.part, a.nblk, 64, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1],
-                                           w.coef + 64);
-    else
+    else if (train) {
+      if (bn_fwd_finalize(sy, 1, w.part, a.nblk, 64, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1],
+                          w.coef + 64, nullptr, s))
+        return -1;
+    } else
       bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN2W], P.p[P_BN2B], rm[1], rv[1], 64, w.coef + 64);
     ABD_LAUNCH_CHECK();
     PoolArgs pa = pool_args(g, 2, B);
@@ -2576,10 +2709,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
                                                   inst_coef + B * 128);
-    else if (train)
-      bn_finalize_kernel<<<32, kT, 0, s>>>(w.part, a.nblk, 32, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2],
-                                           w.coef + 128);
-    else
+    else if (train) {
+      if (bn_fwd_finalize(sy, 2, w.part, a.nblk, 32, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2],
+                          w.coef + 128, nullptr, s))
+        return -1;
+    } else
       bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN3W], P.p[P_BN3B], rm[2], rv[2], 32, w.coef + 128);
     ABD_LAUNCH_CHECK();
     PoolArgs pa = pool_args(g, 3, B);
@@ -2646,7 +2780,7 @@ int loss_and_metrics(abd_cnn* net, const Work& w, const Params& P, const int64_t
 }
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
-             const DropArgs& drop1, hipStream_t s, void* fc_grads_event) {
+             const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{}) {
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -2729,9 +2863,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32 / 4);
     bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
     ABD_LAUNCH_CHECK();
-    bn_bwd_finalize_kernel<<<32, kT, 0, s>>>(w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128,
-                                             G[P_BN3W], G[P_BN3B], w.bcoef + 128);
-    ABD_LAUNCH_CHECK();
+    if (bn_bwd_finalize(sy, 3, w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128, G[P_BN3W],
+                        G[P_BN3B], w.bcoef + 128, s))
+      return -1;
     pa.bcoef = w.bcoef + 128;
     pa.dz = w.dz3;
     pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 32 / 4);
@@ -2760,9 +2894,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
     bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
     ABD_LAUNCH_CHECK();
-    bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64,
-                                             G[P_BN2W], G[P_BN2B], w.bcoef + 64);
-    ABD_LAUNCH_CHECK();
+    if (bn_bwd_finalize(sy, 4, w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64, G[P_BN2W],
+                        G[P_BN2B], w.bcoef + 64, s))
+      return -1;
     pa.bcoef = w.bcoef + 64;
     pa.dz = w.dz2;
     pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 64 / 4);
@@ -2804,9 +2938,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.rows = c1_rows();
     conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
     ABD_LAUNCH_CHECK();
-    bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef,
-                                             G[P_BN1W], G[P_BN1B], w.bcoef);
-    ABD_LAUNCH_CHECK();
+    if (bn_bwd_finalize(sy, 5, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef, G[P_BN1W],
+                        G[P_BN1B], w.bcoef, s))
+      return -1;
     c1.bcoef = w.bcoef;
     abd::prof_begin(abd::PH_CONV1_BWD, s);
     if (g.W1 % 3 == 0)
@@ -2822,13 +2956,14 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   return 0;
 }
 
-DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask) {
+DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask, int64_t cols) {
   DropArgs d{};
   d.enabled = 1;
   d.p = which == 1 ? kP1 : kP2;
   d.scale = 1.0f / (1.0f - d.p);
   d.seed = a->seed;
   d.stream = a->counter * 2 + (uint64_t)(which - 1);
+  d.base = (uint64_t)a->row_offset * (uint64_t)cols;
   d.mask_in = which == 1 ? a->mask1_in : a->mask2_in;
   d.mask_out = ws_mask;
   return d;
@@ -2917,11 +3052,13 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
       P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
   ABD_LAUNCH_CHECK();
-  DropArgs d1 = make_drop(a, 1, w.mask1), d2 = make_drop(a, 2, w.mask2);
-  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked)) return -1;
+  DropArgs d1 = make_drop(a, 1, w.mask1, g.flat), d2 = make_drop(a, 2, w.mask2, 128);
+  const BnSync sy = bn_sync_of(a);
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy))
+    return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
   if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, a->metrics, s)) return -1;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy)) return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
@@ -2947,11 +3084,11 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
   ABD_LAUNCH_CHECK();
   DropArgs d1{}, d2{};
   if (train_mode) {
-    d1 = make_drop(a, 1, w.mask1);
-    d2 = make_drop(a, 2, w.mask2);
+    d1 = make_drop(a, 1, w.mask1, g.flat);
+    d2 = make_drop(a, 2, w.mask2, 128);
   }
   if (forward(net, w, P, a->x, B, a->running, train_mode ? a->running : nullptr, train_mode != 0, d1, d2, s,
-              train_mode ? a->num_batches_tracked : nullptr))
+              train_mode ? a->num_batches_tracked : nullptr, nullptr, train_mode ? bn_sync_of(a) : BnSync{}))
     return -1;
   if (loss_and_metrics(net, w, P, nullptr, nullptr, B, 1.0f, false, w.logp, nullptr, s)) return -1;
   (void)hipMemcpyAsync(a->logprobs_out, w.logp, (size_t)B * g.K * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -2977,7 +3114,7 @@ int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dl
   d1.enabled = 1;
   d1.p = kP1;
   d1.scale = 1.0f / (1.0f - kP1);
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, bn_sync_of(a))) return -1;
   return ABD_OK;
 }
 
@@ -3042,7 +3179,7 @@ int abd_smallcnn_forward_per_utterance(abd_cnn* net, const float* x, int64_t bat
   a.counter = counter;
   a.mask1_in = mask1_in;
   a.mask2_in = mask2_in;
-  DropArgs d1 = make_drop(&a, 1, w.mask1), d2 = make_drop(&a, 2, w.mask2);
+  DropArgs d1 = make_drop(&a, 1, w.mask1, net->g.flat), d2 = make_drop(&a, 2, w.mask2, 128);
   if (forward(net, w, P, x, batch, nullptr, nullptr, true, d1, d2, s, nullptr, icoef)) return -1;
   return loss_and_metrics(net, w, P, nullptr, nullptr, batch, 1.0f, false, logprobs, nullptr, s);
 }

@@ -34,7 +34,7 @@ import torch
 from . import _lib as L
 from . import features as F
 from .io import read_wav_int16, write_wav_int16
-from .models import smallcnn, _draw_seed
+from .models import smallcnn, dropout_seed
 from .triggers import dbfs_int16, db_to_float
 
 N_FRAMES = 32          # daba_selection_tools.py:72-75
@@ -137,7 +137,7 @@ class SelectionModel:
             need = L.lib().abd_smallcnn_forward_per_utterance_workspace_bytes(eng.h, e - s)
             if self._ws is None or self._ws.numel() < need:
                 self._ws = torch.empty(need, dtype=torch.uint8, device=x.device)
-            sd = _draw_seed() if seed is None else seed
+            sd = dropout_seed(x.device) if seed is None else seed
             rc = L.lib().abd_smallcnn_forward_per_utterance(
                 eng.h, x[s:e].data_ptr(), e - s, eng.params.data_ptr(), sd, m._step,
                 mask1[s:e].data_ptr() if mask1 is not None else None,

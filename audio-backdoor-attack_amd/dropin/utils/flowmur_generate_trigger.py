@@ -6,8 +6,4 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import _root  # noqa: F401,E402
 from abd_amd.triggers import deploy_trigger_to_waveform  # noqa: F401,E402
-from abd_amd.flowmur import generate_trigger  # noqa: F401,E402
-
-
-def pretrain_model(train_data, train_label, test_data, test_label, path, num_classes):
-    raise NotImplementedError("use abd_amd.training.clean_train/clean_test with abd_amd.models.smallcnn(K, 224)")
+from abd_amd.flowmur import generate_trigger, pretrain_model  # noqa: F401,E402

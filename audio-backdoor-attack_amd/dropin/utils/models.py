@@ -1,4 +1,10 @@
-"""Drop-in for utils/models.py: smallcnn runs on libabd; the other backbones are out of scope."""
+"""Drop-in for utils/models.py.
+
+``smallcnn`` (utils/models.py:17-65, the BASELINE model) runs on libabd.  The other backbones
+(largecnn, smalllstm, lstmwithattention, RNN, ResNet -- out of scope) are the
+reference's own classes, loaded from the checkout behind this package; the accelerated
+``train()`` / ``test()`` refuse them with an AbdError rather than silently running PyTorch.
+"""
 import os
 import sys
 
@@ -6,16 +12,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import _root  # noqa: F401,E402
 from abd_amd.models import smallcnn  # noqa: F401,E402
 
+from . import reference_module  # noqa: E402
 
-def _unsupported(name):
+_OTHERS = ("largecnn", "smalllstm", "lstmwithattention", "RNN", "ResNet", "ResidualBlock")
+_ref = reference_module("models")
+
+
+def _missing(name):
     def make(*a, **k):
-        raise NotImplementedError(f"{name} is not accelerated by abd_amd (only smallcnn, the BASELINE model)")
+        raise NotImplementedError(f"{name}: no reference utils/models.py on sys.path to take it from "
+                                  "(abd_amd accelerates smallcnn only)")
     return make
 
 
-largecnn = _unsupported("largecnn")
-smalllstm = _unsupported("smalllstm")
-lstmwithattention = _unsupported("lstmwithattention")
-RNN = _unsupported("RNN")
-ResNet = _unsupported("ResNet")
-ResidualBlock = _unsupported("ResidualBlock")
+for _n in _OTHERS:
+    globals()[_n] = getattr(_ref, _n) if _ref is not None and hasattr(_ref, _n) else _missing(_n)

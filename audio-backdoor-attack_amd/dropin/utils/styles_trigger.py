@@ -1,4 +1,5 @@
-"""Drop-in for utils/styles_trigger.py: pedalboard effects are not accelerated yet (§8f item 4)."""
+"""Drop-in for utils/styles_trigger.py: the pedalboard boards run as libabd kernels (csrc/effects.hip);
+PitchShift boards (styles 0 and 3) raise AbdError."""
 import os
 import sys
 

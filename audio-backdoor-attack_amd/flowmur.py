@@ -177,3 +177,38 @@ def generate_trigger(benign_model, dataloader, trigger_length, path, num_epoch=3
     if verbose:
         print("last trigger:", opt.trigger[None])
     return opt.trigger[None].detach().clone()
+
+
+def pretrain_model(train_data, train_label, test_data, test_label, path, num_classes, max_epochs=1000, runs=3,
+                   device=None):
+    """Surrogate (benign) model pretraining, utils/flowmur_generate_trigger.py:15-47: 80/20 validation
+    split (random_state 35), three smallcnn(num_classes, 224) runs of clean_train / clean_test with
+    EarlyStoppingModel(patience 20) checkpoints ``<path>/smallcnn_<K>_<i>.pkl``, then the last run's
+    checkpoint scored on the test set.  Returns that checkpoint's path (what flowmur.py:53-55 loads)."""
+    from sklearn.model_selection import train_test_split
+    from . import training as T
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    tr_x, va_x, tr_y, va_y = train_test_split(train_data, train_label, test_size=0.2, random_state=35)
+    as_t = lambda a: torch.as_tensor(np.asarray(a))  # noqa: E731
+    mk = lambda x, y: torch.utils.data.DataLoader(torch.utils.data.TensorDataset(as_t(x), as_t(y)),  # noqa: E731
+                                                  batch_size=256, shuffle=True)
+    train_loader, val_loader, test_loader = mk(tr_x, tr_y), mk(va_x, va_y), mk(test_data, test_label)
+    criterion = torch.nn.CrossEntropyLoss()
+    save_path = None
+    for i in range(runs):
+        model = smallcnn(num_classes, 224).to(dev)
+        opt = torch.optim.Adam(model.parameters(), lr=0.0001)
+        save_path = os.path.join(path, f"smallcnn_{num_classes}_{i}.pkl")
+        es = T.EarlyStoppingModel(patience=20, verbose=True, path=save_path)
+        for epoch in range(1, max_epochs + 1):
+            train_loss, train_acc = T.clean_train(model, train_loader, dev, opt, criterion)
+            val_loss, val_acc = T.clean_test(model, dev, val_loader, criterion)
+            es(val_loss, model=model)
+            print(f"Epoch {epoch}: Train loss: {train_loss:.4f}, Train acc: {train_acc:.4f}, Val acc: {val_acc:.4f}")
+            if es.early_stop:
+                print("Early stopping")
+                break
+    benign = torch.load(save_path, map_location=dev, weights_only=False)   # our own checkpoint
+    test_loss, test_acc = T.clean_test(benign, dev, test_loader, criterion)
+    print(f"Test loss: {test_loss:.4f}, Test acc: {test_acc:.4f}")
+    return save_path

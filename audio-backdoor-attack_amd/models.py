@@ -87,9 +87,28 @@ class _Engine:
             pass
 
 
-def _draw_seed() -> int:
-    # consume the torch CPU generator (reproducible under fix_random())
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+def dropout_seed(device) -> int:
+    """Seed of the device dropout hash: the device's default torch generator seed (set by
+    torch.manual_seed / fix_random(), utils/random_tools.py:5-18).  Nothing is drawn from the
+    global CPU generator, as on the reference's CUDA path where nn.Dropout consumes the device
+    generator and the CPU stream only feeds the DataLoader shuffles -- so the batch order of
+    every epoch matches the reference's under the same seed."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    return int(torch.cuda.default_generators[idx].initial_seed()) & ((1 << 63) - 1)
+
+
+DROPOUT_SOURCES = ("device", "torch_cpu")
+
+
+def torch_cpu_masks(batch: int, flat: int, device):
+    """Dropout keep-masks drawn exactly as the reference's CPU forward draws them: nn.Dropout(0.4)
+    then nn.Dropout(0.5) (utils/models.py:55,60) each call bernoulli_(1 - p) on a tensor of the
+    input's shape from the global CPU generator (ATen's non-fused CPU dropout); the draw does not
+    depend on the shape, only on the element count, so (B, flat) reproduces (B, 32, H, W)."""
+    m1 = torch.empty((batch, flat)).bernoulli_(0.6).to(torch.uint8)
+    m2 = torch.empty((batch, 128)).bernoulli_(0.5).to(torch.uint8)
+    return m1.to(device, non_blocking=True), m2.to(device, non_blocking=True)
 
 
 class smallcnn(nn.Module):
@@ -115,11 +134,30 @@ class smallcnn(nn.Module):
         self._engine = None
         self._step = 0
         self.gemm_precision = "f32"   # "bf16": conv GEMMs on bf16 MFMA (set_gemm_precision)
+        self.dropout_source = "device"  # "torch_cpu": the reference CPU path's exact masks
+
+    def set_dropout_source(self, source: str):
+        """'device' (default): keep-masks from a counter-based hash on the GPU, seeded by the device
+        generator.  'torch_cpu': the masks the reference's CPU forward would draw from the global CPU
+        generator (torch_cpu_masks), copied to the device each step -- a whole run then consumes the
+        CPU RNG stream exactly like the reference CPU path, batch order included (parity runs)."""
+        if source not in DROPOUT_SOURCES:
+            raise ValueError(f"dropout source must be one of {DROPOUT_SOURCES}, got {source!r}")
+        self.dropout_source = source
+        return self
+
+    def step_masks(self, batch: int, device):
+        """Host-drawn masks for the next train-mode forward, or None (device hash)."""
+        if getattr(self, "dropout_source", "device") != "torch_cpu":
+            return None
+        return torch_cpu_masks(batch, self.fc1.in_features, device)
 
     def __getstate__(self):
         # the libabd handle is process-local; parameters pickle as ordinary tensors
         st = self.__dict__.copy()
         st["_engine"] = None
+        st.pop("_host_masks", None)
+        st.pop("_capture_masks", None)
         return st
 
     # ------------------------------------------------------------------ binding
@@ -214,9 +252,14 @@ class smallcnn(nn.Module):
             return out
         a = self._args(eng, x, B)
         a.logprobs_out = out.data_ptr()
-        a.seed = _draw_seed() if seed is None else seed
+        a.seed = dropout_seed(x.device) if seed is None else seed
         a.counter = self._step
         self._step += 1
+        if mask1 is None:
+            hm = self.step_masks(B, x.device)
+            if hm is not None:
+                mask1, mask2 = hm
+                self._host_masks = hm  # keep alive until the launch has consumed them
         if mask1 is not None:
             a.mask1_in, a.mask2_in = mask1.data_ptr(), mask2.data_ptr()
         masks_out = masks_out if masks_out is not None else getattr(self, "_capture_masks", None)

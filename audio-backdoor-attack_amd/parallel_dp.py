@@ -72,6 +72,52 @@ class OverlappedGradAllReduce:
         return self.flat
 
 
+def broadcast_state(tensors, src: int = 0, group=None):
+    """Make every rank start from (or return to) rank src's model state: the flat parameter
+    buffer and the packed BN running statistics (DDP's init broadcast + broadcast_buffers)."""
+    for t in tensors:
+        if t is not None:
+            dist.broadcast(t, src=src, group=group)
+
+
+class SyncBatchNorm:
+    """Synchronised BatchNorm statistics for the fused train step (abd_train_args.bn_sync*).
+
+    The reference normalises over its whole batch (utils/models.py:20-30 in train mode); with
+    per-rank statistics an N-GPU step differs from the 1-process step on the same global batch.
+    libabd calls ``_sync`` six times per step (3 forward statistic reductions, 3 backward) with
+    this rank's per-channel double sums (2C+1 values: sums, sums of squares / products, element
+    count) written into ``buf``; the callback sums them over ranks with an all-reduce enqueued on
+    the current stream (RCCL on the GPU box, gloo in rehearsals), and the kernels that follow use
+    the global sums and count.  129 doubles per call: latency-bound, ~6 x 10 us on xGMI.
+    """
+
+    def __init__(self, device, group=None):
+        from . import _lib as L
+        self.group = group
+        self.buf = torch.zeros(6 * L.BN_SYNC_STRIDE, dtype=torch.float64, device=device)
+        self.calls = 0
+        self.error = None
+
+        def _sync(ctx, point, offset, n):
+            try:
+                dist.all_reduce(self.buf[offset:offset + n], op=dist.ReduceOp.SUM, group=self.group)
+                self.calls += 1
+                return 0
+            except Exception as e:  # surfaced as an AbdError by the launch's return code
+                self.error = e
+                return 1
+
+        self._cb = L.BN_SYNC_FN(_sync)   # keep the ctypes thunk alive as long as this object
+        import ctypes as C
+        self._cb_ptr = C.cast(self._cb, C.c_void_p).value
+
+    def bind(self, args):
+        args.bn_sync_buf = self.buf.data_ptr()
+        args.bn_sync = self._cb_ptr
+        args.bn_sync_ctx = None
+
+
 def reduce_metrics(m: torch.Tensor, group=None) -> torch.Tensor:
     """Combine libabd metric words across ranks: counts summed, batch-mean loss averaged.
 

@@ -83,10 +83,72 @@ def attack_config(name: str, **kw) -> AttackConfig:
     return c
 
 
+def poison_schedule(cfg: AttackConfig, labels: np.ndarray, seed: int = 35, trigger_len: int | None = None):
+    """The reference's poisoning index work, reproduced exactly under fix_random() (seed 35).
+
+    Returns (poison_rows, positions, pyrand): the poisoned training rows in the order the reference
+    visits them, the FlowMur window start of each (None for the other attacks) and the python
+    Random whose stream continues into the test-set draws.
+      * badnets / ultrasonic / jingleback: ``random.sample(range(N), int(N * rate))``
+        (badnets.py:50-51, ultrasonic.py:70-71, jingleback.py:66-67);
+      * flowmur: ``random.sample(range(n_train_split), 5000)`` (flowmur.py:58-60; it needs >= 5000
+        rows after the 80/20 validation split -- skipped below that, where the reference raises),
+        ``np.random.choice(target_rows, int(n_target * rate), replace=False)`` (:74-76, numpy's
+        legacy global RandomState seeded by fix_random) and one ``random.randint(0, L - Lt)`` per
+        poisoned clip in that order (:78-81).
+    """
+    import random
+    N = int(labels.shape[0])
+    pyrand = random.Random(seed)
+    if cfg.clean_label:
+        n_tr = N - int(math.ceil(0.2 * N))          # train_test_split(test_size=0.2) train rows
+        if n_tr >= 5000:
+            pyrand.sample(range(n_tr), 5000)
+        target = np.where(labels == cfg.target_label)[0]
+        k = int(target.shape[0] * cfg.poisoning_rate)
+        rows = np.random.RandomState(seed).choice(target, k, replace=False)
+        span = cfg.length - int(trigger_len)
+        pos = np.array([pyrand.randint(0, span) for _ in rows], dtype=np.int64)
+        return rows.astype(np.int64), pos, pyrand
+    rows = np.array(pyrand.sample(range(N), int(N * cfg.poisoning_rate)), dtype=np.int64)
+    return rows, None, pyrand
+
+
 def ultrasonic_trigger(size=60, pos="mid", cont=False) -> np.ndarray:
     """GenerateTrigger(size, pos, cont).trigger()[0] (utils/ultra_trigger.py:26-111) from the packaged samples."""
     from .triggers import GenerateTrigger
     return GenerateTrigger(size, pos, cont=cont).trigger()[0].astype(np.float32)
+
+
+class LoaderOrder:
+    """Epoch orders of ``DataLoader(train_set, batch_size, shuffle=True)`` (badnets.py:107,
+    ultrasonic.py:136, jingleback.py:131, daba.py:152, flowmur.py:91) under fix_random().
+
+    Each epoch's iterator draws its base seed (``_BaseDataLoaderIter``), then ``RandomSampler``
+    its permutation seed, from the torch CPU stream; between two training epochs ``eval_model``
+    runs ``test()`` over two shuffled loaders (two more draws each).  On the reference's GPU path
+    nothing else consumes that stream (dropout draws from the device generator), so epoch e's
+    order is reproduced from a private generator seeded like ``torch.manual_seed(seed)``."""
+
+    def __init__(self, n: int, seed: int = 35, test_loaders_per_epoch: int = 2):
+        self.n = int(n)
+        self.gen = torch.Generator()
+        self.gen.manual_seed(seed)
+        self.test_loaders = int(test_loaders_per_epoch)
+        self.epochs = 0
+
+    def _draw(self) -> int:
+        return int(torch.empty((), dtype=torch.int64).random_(generator=self.gen).item())
+
+    def next_epoch(self) -> torch.Tensor:
+        if self.epochs > 0:
+            for _ in range(2 * self.test_loaders):
+                self._draw()
+        self._draw()                      # _BaseDataLoaderIter._base_seed
+        g = torch.Generator()
+        g.manual_seed(self._draw())       # RandomSampler.__iter__
+        self.epochs += 1
+        return torch.randperm(self.n, generator=g)
 
 
 class ResidentTrainer:
@@ -94,8 +156,11 @@ class ResidentTrainer:
 
     def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
                  optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
-                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None, overlap_features: bool = False,
-                 gemm_precision: str | None = None):
+                 seed: int = 35, rank: int = 0, world: int = 1, process_group=None,
+                 gemm_precision: str | None = None, sync_bn: bool = False, poison_rows=None):
+        """batch_size is per rank (global batch = batch_size * world).  poison_rows: explicit
+        poisoned rows (e.g. DABA's file-level schedule); default: the reference's own index work
+        (poison_schedule).  sync_bn: BatchNorm statistics over the global batch (world > 1)."""
         assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
         self.cfg, self.model, self.opt = cfg, model, optimizer
         self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
@@ -104,14 +169,14 @@ class ResidentTrainer:
         self.labels = labels.to(self.dev, torch.int64)
         N = waves.shape[0]
         self.N = N
-        rng = np.random.Generator(np.random.PCG64(seed))
         lab_np = self.labels.cpu().numpy()
-        if cfg.clean_label:  # flowmur.py:74-76 / :88-89
-            cand = np.nonzero(lab_np == cfg.target_label)[0]
-            pois = rng.choice(cand, int(cand.size * cfg.poisoning_rate), replace=False)
+        tlen = len(trigger) if trigger is not None else None
+        pois, wpos, self._pyrand = poison_schedule(cfg, lab_np, seed, tlen)
+        if poison_rows is not None:
+            pois, wpos = np.asarray(poison_rows, dtype=np.int64), None
+        if cfg.clean_label:  # flowmur.py:88-89: every target-class clip counts for the train ASR
             ind = (lab_np == cfg.target_label).astype(np.int64)
-        else:  # random.sample(indices, int(N * rate)) (badnets.py:110)
-            pois = rng.choice(N, int(N * cfg.poisoning_rate), replace=False)
+        else:                # badnets.py:53-61
             ind = np.zeros(N, np.int64)
             ind[pois] = 1
         pmask = np.zeros(N, np.uint8)
@@ -124,10 +189,16 @@ class ResidentTrainer:
         self.eff_labels = torch.tensor(eff, device=self.dev)
         self.trigger = torch.tensor(trigger, dtype=torch.float32, device=self.dev) if trigger is not None else None
         if cfg.inject_mode in (L.INJECT_SNR_WINDOW, L.INJECT_HALF_MIX, L.INJECT_DEPLOY):
-            span = cfg.length - self.trigger.numel()
-            self.position = torch.tensor(rng.integers(0, span + 1, N), dtype=torch.int32, device=self.dev)
+            pos_all = np.zeros(N, np.int32)
+            if wpos is not None:
+                pos_all[pois] = wpos
+            else:
+                span = cfg.length - self.trigger.numel()
+                pos_all[pois] = [self._pyrand.randint(0, span) for _ in pois]
+            self.position = torch.tensor(pos_all, dtype=torch.int32, device=self.dev)
         else:
             self.position = None
+        self._test_pos = {}
         self.board = None
         self.src_row = None
         if cfg.style is not None:
@@ -149,108 +220,81 @@ class ResidentTrainer:
         model.train()
         if gemm_precision is not None:
             model.set_gemm_precision(gemm_precision)
-        model.engine(self.x)
+        eng = model.engine(self.x)
         self.adam = T.AdamBinding(model, optimizer)
-        self.gen = torch.Generator()
-        self.gen.manual_seed(seed)
+        self.order = LoaderOrder(N, seed)
         self._epoch = None
         self._pos = 0
         self.reducer = None
+        self.bn_sync = None
         if world > 1:
-            split = int(model._engine.offsets[12])  # fc1.weight onwards (P_F1W)
-            self.reducer = DP.OverlappedGradAllReduce(model._engine.grads, split, process_group)
-
-        # optional feature prefetch: batch k+1's inject + MFCC on a side stream while batch k trains,
-        # two feature buffers, events order reuse.  Off by default: measured on MI355X (B = 512,
-        # ultrasonic) it gains nothing -- the persistent STFT kernel and the conv GEMMs do not
-        # co-reside usefully on the CUs -- and at N > 1 it adds a stream beside RCCL's.
-        self.overlap = bool(overlap_features)
-        self.xbuf = [self.x, torch.empty_like(self.x)] if self.overlap else [self.x]
-        if self.overlap:
-            self.feat_stream = torch.cuda.Stream(self.dev)
-            self.feat_ready = [torch.cuda.Event(), torch.cuda.Event()]
-            self.buf_free = [torch.cuda.Event(), torch.cuda.Event()]
-        self._ahead = None      # (buffer, batch) whose features are already enqueued
-        self._nbuf = 0
-        self._epoch_event = None
+            # DDP semantics: every rank starts from rank 0's parameters and BN buffers
+            DP.broadcast_state([eng.params, eng.running, eng.nbt], 0, process_group)
+            split = int(eng.offsets[12])  # fc1.weight onwards (P_F1W)
+            self.reducer = DP.OverlappedGradAllReduce(eng.grads, split, process_group)
+            if sync_bn:
+                self.bn_sync = DP.SyncBatchNorm(self.dev, process_group)
 
     # -------------------------------------------------------------- epoch plumbing
     def new_epoch(self):
-        perm = torch.randperm(self.N, generator=self.gen).to(self.dev)
+        perm = self.order.next_epoch().to(self.dev)
         rows = self.src_row[perm] if self.src_row is not None else perm.to(torch.int32)
         self._epoch = (rows, self.eff_labels[perm], self.ind[perm], self.poison[perm],
                        self.position[perm] if self.position is not None else None)
         self._pos = 0
-        self._ahead = None  # a prefetched batch of the previous epoch is dropped
-        if self.overlap:
-            self._epoch_event = torch.cuda.Event()
-            self._epoch_event.record()
+
+    def _batch_rows(self, pos):
+        """Rows of the global batch starting at pos: a full B * world, or (one rank) the loader's
+        short last batch (drop_last=False); None when the epoch is spent."""
+        G = self.B * self.world
+        left = self.N - pos
+        if left >= G:
+            return G
+        if self.world == 1 and left >= 2:   # BatchNorm needs two rows; a 1-row tail is dropped
+            return left
+        return None
 
     def steps_per_epoch(self):
-        return self.N // (self.B * self.world)
+        n, pos = 0, 0
+        while self._batch_rows(pos) is not None:
+            pos += self._batch_rows(pos)
+            n += 1
+        return n
 
     def _take_batch(self):
-        """This rank's slices of the next global batch (starting a new epoch when the current one is spent)."""
-        if self._epoch is None or self._pos + self.B * self.world > self.N:
+        """This rank's slice of the next global batch (starting a new epoch when the current one is spent)."""
+        if self._epoch is None or self._batch_rows(self._pos) is None:
             self.new_epoch()
+        g = self._batch_rows(self._pos)
+        b = g // self.world
         rows, lab, ind, pois, pos = self._epoch
-        s, e = DP.shard_slice(self._pos, self.B, self.rank, self.world)
-        self._pos += self.B * self.world
+        s, e = DP.shard_slice(self._pos, b, self.rank, self.world)
+        self._pos += g
         return rows[s:e], lab[s:e], ind[s:e], pois[s:e], pos[s:e] if pos is not None else None
 
-    def _features(self, batch, out, stream=None):
+    def _features(self, batch, out):
         rows, _, _, pois, pos = batch
         inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois, position=pos,
                           snr_db=self.cfg.snr_db, patch=self.cfg.patch)
-        if stream is None:
-            F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
-            return
-        for t in (rows, pois, pos):
-            if t is not None:
-                t.record_stream(stream)
-        with torch.cuda.stream(stream):
-            F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
+        F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
 
-    def _prefetch(self):
-        """Enqueue the next batch's features on the feature stream into the other buffer."""
-        i = self._nbuf
-        batch = self._take_batch()
-        fs = self.feat_stream
-        if self._epoch_event is not None:
-            fs.wait_event(self._epoch_event)
-            self._epoch_event = None
-        fs.wait_event(self.buf_free[i])   # the train step that last read buffer i has finished
-        self._features(batch, self.xbuf[i], fs)
-        self.feat_ready[i].record(fs)
-        self._ahead = (i, batch)
-        self._nbuf ^= 1
-
-    def step(self, prefetch_next: bool = True):
+    def step(self):
         """One global batch: this rank's slice through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
-        if not self.overlap:
-            batch = self._take_batch()
-            self._features(batch, self.x)
-            self._train(batch)
-            return
-        if self._ahead is None:
-            self._prefetch()
-        i, batch = self._ahead
-        self._ahead = None
-        if prefetch_next:
-            self._prefetch()              # batch k+1's features overlap batch k's training
-        torch.cuda.current_stream(self.dev).wait_event(self.feat_ready[i])
-        self.x = self.xbuf[i]
-        self._train(batch)
-        self.buf_free[i].record()
+        batch = self._take_batch()
+        b = batch[0].numel()
+        x = self.x if b == self.B else self.x[:b]
+        self._features(batch, x)
+        self._train(batch, x)
 
-    def _train(self, batch):
+    def _train(self, batch, x):
         _, lab, ind, _, _ = batch
         if self.world == 1:
-            T.train_step(self.model, self.x, lab, ind, self.adam, self.metrics)
+            T.train_step(self.model, x, lab, ind, self.adam, self.metrics)
         else:
-            T.train_step(self.model, self.x, lab, ind, self.adam, self.metrics, do_update=False,
+            T.train_step(self.model, x, lab, ind, self.adam, self.metrics, do_update=False,
                          grad_scale=DP.grad_scale(self.B, self.B * self.world),
-                         fc_grads_event=self.reducer.event_ptr())
+                         fc_grads_event=self.reducer.event_ptr(), row_offset=self.rank * self.B,
+                         bn_sync=self.bn_sync)
             self.reducer.launch_fc()   # fc grads all-reduce overlaps the conv backward
             self.reducer.finish()      # conv head all-reduce, join
             T.apply_adam(self.model, self.adam, self.dev)
@@ -258,9 +302,8 @@ class ResidentTrainer:
     def run_epoch(self):
         self.new_epoch()
         self.metrics.zero_()
-        n = self.steps_per_epoch()
-        for k in range(n):
-            self.step(prefetch_next=k + 1 < n)  # never draw the next epoch's permutation early
+        for _ in range(self.steps_per_epoch()):
+            self.step()
         return self.read_metrics()
 
     def read_metrics(self, reduce=True):
@@ -271,35 +314,68 @@ class ResidentTrainer:
         return {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
                 "asr": 100.0 * ah / max(pt, 1), "samples": total, "poisoned": pt}
 
+    def sync_buffers(self):
+        """DDP broadcast_buffers: BN running statistics from rank 0 (evaluation and checkpoints see
+        one model on every rank; with sync_bn they are already identical)."""
+        if self.world > 1:
+            eng = self.model._engine
+            DP.broadcast_state([eng.running, eng.nbt], 0, self.pg)
+
     # -------------------------------------------------------------- evaluation (test(), training_tools.py:87-134)
+    def bd_test_set(self, labels: torch.Tensor):
+        """(rows, poisoned, positions) of the backdoor test set built from clean test clips.
+
+        badnets / ultrasonic / jingleback (badnets.py:66-77, ultrasonic.py:90-102): every test clip;
+        target-class clips stay clean with indicator 0, the others are poisoned with indicator 1;
+        all labels are the target.  flowmur (flowmur.py:98-109): target-class clips dropped, the
+        rest mixed as (w + t)/2 in a window at random.randint(0, L - Lt) (drawn once per test set,
+        continuing the training schedule's python stream), w/2 outside; indicator 1."""
+        lab = labels.to(self.dev, torch.int64)
+        idx = torch.arange(lab.numel(), device=self.dev)
+        if self.cfg.clean_label:
+            rows = idx[lab != self.cfg.target_label]
+            key = (int(lab.numel()), int(rows.numel()))
+            if key not in self._test_pos:
+                span = self.cfg.length - self.trigger.numel()
+                self._test_pos[key] = torch.tensor([self._pyrand.randint(0, span) for _ in range(rows.numel())],
+                                                   dtype=torch.int32, device=self.dev)
+            return rows, torch.ones(rows.numel(), dtype=torch.bool, device=self.dev), self._test_pos[key]
+        return idx, lab != self.cfg.target_label, None
+
     @torch.no_grad()
     def evaluate(self, waves: torch.Tensor, labels: torch.Tensor, batch: int = 512):
-        """Clean accuracy on (waves, labels); ASR on the non-target clips with the trigger injected."""
+        """test(): clean accuracy / loss on (waves, labels), ASR / loss on the backdoor test set
+        (bd_test_set).  Losses are means of per-batch mean losses over `batch`-row batches."""
+        self.sync_buffers()
         self.model.eval()
         eng = self.model._engine
         labels = labels.to(self.dev, torch.int64)
+        bd_rows, bd_pois, bd_pos = self.bd_test_set(labels)
+        test_mode = L.INJECT_HALF_MIX if self.cfg.clean_label else self.cfg.inject_mode
         res = {}
-        for name, poisoned in (("clean", False), ("bd", True)):
-            idx = torch.arange(waves.shape[0], device=self.dev)
-            if poisoned:
-                idx = idx[labels != self.cfg.target_label]
+        for name in ("clean", "bd"):
+            rows_all = torch.arange(labels.numel(), device=self.dev) if name == "clean" else bd_rows
             m = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
-            for s in range(0, idx.numel(), batch):
-                rows = idx[s:s + batch].to(torch.int32)
+            for s in range(0, rows_all.numel(), batch):
+                rows = rows_all[s:s + batch].to(torch.int32)
                 B = rows.numel()
-                pois = torch.ones(B, dtype=torch.uint8, device=self.dev) if poisoned else None
-                pos = self.position[rows.long() % self.N] if (poisoned and self.position is not None) else None
-                inj = F.Injection(mode=self.cfg.inject_mode if poisoned else L.INJECT_NONE, trigger=self.trigger,
-                                  poison=pois, position=pos, snr_db=self.cfg.snr_db,
-                                  patch=self.cfg.patch if poisoned else None)
-                if poisoned and self.board is not None:
-                    styled = self.board.apply_device(waves, self.cfg.sample_rate, rows=rows)
-                    x = F.mfcc_batch(styled, self.mcfg, inject=inj)
+                if name == "clean":
+                    x = F.mfcc_batch(waves, self.mcfg, rows=rows)
+                    y, ind = labels[rows.long()], None
                 else:
-                    x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
-                y = torch.full((B,), self.cfg.target_label, dtype=torch.int64, device=self.dev) if poisoned \
-                    else labels[rows.long()]
-                ind = torch.ones(B, dtype=torch.int64, device=self.dev) if poisoned else None
+                    pois = bd_pois[s:s + batch]
+                    inj = F.Injection(mode=test_mode, trigger=self.trigger, poison=pois.to(torch.uint8),
+                                      position=bd_pos[s:s + batch] if bd_pos is not None else None,
+                                      snr_db=self.cfg.snr_db, patch=self.cfg.patch)
+                    if self.board is not None:   # jingleback.py:94-104: styled non-target clips
+                        src = waves[rows.long()]
+                        styled = self.board.apply_device(waves, self.cfg.sample_rate, rows=rows)
+                        src = torch.where(pois[:, None], styled, src).contiguous()
+                        x = F.mfcc_batch(src, self.mcfg, inject=inj)
+                    else:
+                        x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
+                    y = torch.full((B,), self.cfg.target_label, dtype=torch.int64, device=self.dev)
+                    ind = pois.to(torch.int64)
                 out = torch.empty((B, eng.K), device=self.dev)
                 ws = eng.workspace(B)
                 L.check(L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(),
@@ -309,6 +385,6 @@ class ResidentTrainer:
                         "abd_smallcnn_eval")
             loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
             res[name] = {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
-                         "asr": 100.0 * ah / max(pt, 1)}
+                         "asr": 100.0 * ah / max(pt, 1), "samples": total, "poisoned": pt}
         self.model.train()
         return res

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .models import smallcnn, _draw_seed
+from .models import smallcnn, dropout_seed
 
 
 # ------------------------------------------------------------------ Adam state shared with torch
@@ -74,8 +74,11 @@ def _as_long(t, device):
 
 def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None, metrics: torch.Tensor | None,
                mask1=None, mask2=None, masks_out=None, do_update=True, grad_scale=1.0, seed=None, logprobs_out=None,
-               fc_grads_event=None):
-    """One fused device step (forward + CE + backward [+ Adam]) -- the per-batch hot path."""
+               fc_grads_event=None, row_offset=0, bn_sync=None):
+    """One fused device step (forward + CE + backward [+ Adam]) -- the per-batch hot path.
+
+    row_offset: global batch row of x[0] (data parallelism: dropout masks hash the global row).
+    bn_sync: a parallel_dp.SyncBatchNorm (synchronised BatchNorm statistics) or None."""
     eng = model.engine(x)
     B = x.shape[0]
     a = model._args(eng, x, B)
@@ -88,9 +91,16 @@ def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None,
             adam.step += 1
             a.adam_step = adam.step
             a.do_update = 1
-    a.seed = _draw_seed() if seed is None else seed
+    a.seed = dropout_seed(x.device) if seed is None else seed
     a.counter = model._step
     model._step += 1
+    a.row_offset = int(row_offset)
+    if bn_sync is not None:
+        bn_sync.bind(a)
+    if mask1 is None:
+        hm = model.step_masks(B, x.device)
+        if hm is not None:
+            mask1, mask2 = hm
     if mask1 is not None:
         a.mask1_in, a.mask2_in = mask1.data_ptr(), mask2.data_ptr()
     if masks_out is not None:
@@ -156,7 +166,8 @@ def train(model, train_loader, device, optimizer, criterion):
     if adam is not None:
         adam.sync_torch_state()
         expose_grads(model)
-    loss_sum, total, correct, ptotal, asr = read_metrics(metrics)
+    loss_sum, total, correct, ptotal, asr, _ = read_metrics(metrics)
+    # train_loss = running_loss / len(train_loader): the sum of per-batch loss.item() values
     return loss_sum / nbatches, 100.0 * correct / total, 100 * asr / ptotal
 
 

@@ -4,7 +4,7 @@
 * Ultrasonic ``GenerateTrigger`` / ``TriggerInfeasible``        utils/ultra_trigger.py:8-111
 * FlowMur  ``deploy_trigger_to_waveform``                       utils/flowmur_generate_trigger.py:49-62
 * DABA     ``single_trigger_injection_db`` on int16 arrays      utils/daba_selection_tools.py:24-39
-* JingleBack ``get_boards`` / ``poison_style``                  utils/styles_trigger.py:8-53 (not accelerated)
+* JingleBack ``get_boards`` / ``poison_style``                  utils/styles_trigger.py:8-53 (libabd effects kernels; PitchShift raises)
 
 Trigger *construction* is a one-off host computation (microseconds, once per run);
 trigger *application* per batch happens inside libabd's feature kernel

@@ -110,44 +110,93 @@ def load_traffic(phase):
     return None
 
 
-def cpu_baseline(n, threads):
-    """The float64 numpy oracle (port of the reference path) on a bounded sample, host cores."""
+def cpu_threads():
+    """Host threads for the CPU baseline: this process's CPU affinity, capped by OMP_NUM_THREADS
+    (the GPU box exports 16, its CPU share; its affinity mask shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_baseline(batch, threads, steps=2):
+    """The reference CPU path at the bench's batch: torch-fp32 restatement
+    (oracle/torch_ref.py: torch.stft MFCC with torchaudio's semantics + nn smallcnn with the
+    reference structure + torch Adam), ultrasonic K=35, 10 % poisoned; 1 warmup + `steps` timed."""
     import numpy as np
-    from threadpoolctl import threadpool_limits
+    import torch
+    from oracle import torch_ref
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from golden_inputs import ultrasonic_trigger_f32
     from abd_amd import synth
-    from abd_amd.pipeline import ultrasonic_trigger
-    from oracle import mfcc as om, smallcnn as oc
-    from tests.golden_inputs import make_state
-    w, lab = synth.make_clips_np(n, 44100, 44100, 35, seed=123)
-    trig = ultrasonic_trigger(60, "mid", False).astype(np.float64)
-    r = np.random.Generator(np.random.PCG64(1))
-    pois = r.random(n) < 0.1
-    lab = np.where(pois, 2, lab)
-    with threadpool_limits(limits=threads):
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        n = 2 * batch
+        w, lab = synth.make_clips_np(n, 44100, 44100, 35, seed=123)
+        waves, labels = torch.from_numpy(w), torch.from_numpy(lab)
+        trig = torch.from_numpy(ultrasonic_trigger_f32()[0])
+        feat = torch_ref.MfccCPU(44100, 40, 1103, 441)
+        torch.manual_seed(5)
+        model = torch_ref.SmallCNN(35, 3072).train()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+        g = torch.Generator().manual_seed(1)
+
+        def step():
+            rows = torch.randint(0, n, (batch,), generator=g)
+            pois = torch.rand(batch, generator=g) < 0.1
+            x = waves[rows] + pois[:, None].float() * trig[None]      # ultrasonic.py:75 (poisoned rows)
+            y = torch.where(pois, torch.full_like(labels[rows], 2), labels[rows])
+            return torch_ref.train_step(model, opt, feat(x), y, pois.long())
+        step()
         t0 = time.perf_counter()
-        ww = w.astype(np.float64)
-        ww[pois] += trig[None]
-        x = om.mfcc_model_input(ww, 44100, 40, 1103, 441)
-        m = oc.SmallCNN(make_state(100, 40, 35, 3072, seed=5))
-        m.train_step(x, lab, r.random((n, 3072)) < 0.6, r.random((n, 128)) < 0.5)
+        for _ in range(steps):
+            step()
         dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 2), "unit": "utterances/s", "cores": threads, "kind": "port",
-            "sample": f"{n} ultrasonic utterances (44.1 kHz x 1 s): trigger add + MFCC(1103/441) + one smallcnn "
-                      f"train step (fwd/bwd/Adam), float64 numpy oracle, {dt:.1f} s"}
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(batch * steps / dt, 2), "unit": "utterances/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} steps of batch {batch} after 1 warmup ({dt:.1f} s): ultrasonic clips (44.1 kHz x 1 s), "
+                      "trigger add + torch.stft MFCC(1103/441) + smallcnn fwd/bwd/Adam in torch fp32 on the host "
+                      "(oracle/torch_ref.py, the reference CPU path restated)"}
+
+
+FEATURE_PHASES = ("stft_mel", "db_dct")
+
+
+def feature_bytes(L, T, C):
+    """SURVEY §8(d) algorithmic bytes per utterance of the feature stage: wave read + MFCC write."""
+    return 4.0 * L + 4.0 * T * C
+
+
+def train_flops(H0, W0, K):
+    """3 F_fwd - F_conv1 per utterance (conv + linear, 2 FLOP per MAC)."""
+    H1, W1 = H0 - 1, W0 - 1
+    W1p = W1 // 3
+    H2, W2 = H1 - 1, W1p - 1
+    H2p, W2p = H2 // 2 + 1, W2 // 2 + 1
+    H3, W3 = H2p - 1, W2p - 1
+    H3p, W3p = (H3 - 2) // 2 + 1, W3 // 2 + 1
+    flat = 32 * H3p * W3p
+    c1 = 2.0 * H1 * W1 * 64 * 4
+    fwd = c1 + 2.0 * H2 * W2 * 64 * 256 + 2.0 * H3 * W3 * 32 * 256 + 2.0 * flat * 128 + 2.0 * 128 * K
+    return 3.0 * fwd - c1
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch (configs[1]: bs=512)")
-    ap.add_argument("--n-train", type=int, default=8192, help="resident training clips per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=192, help="utterances for the CPU baseline (0 = skip)")
+    ap.add_argument("--n-train", type=int, default=8192, help="resident training clips per GPU (the table is "
+                    "replicated on every rank and holds n_train x world clips, so an epoch has the same number "
+                    "of steps at every N)")
+    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps at the bench batch (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
+    ap.add_argument("--windows", type=int, default=5, help="equal windows of the timed steps (median reported)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo for 1-GPU rehearsal")
-    ap.add_argument("--overlap", action="store_true", help="prefetch the next batch's features on a side stream")
+    ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over the global batch")
     ap.add_argument("--attack", default="ultrasonic", help="workload: ultrasonic (headline, configs[1]), badnets, "
                     "jingleback, daba, flowmur")
     ap.add_argument("--gemm-precision", default="f32split", choices=("f32", "f32split", "bf16"),
@@ -182,9 +231,10 @@ def main():
     cfg = attack_config(args.attack)
     headline = args.attack == "ultrasonic" and args.gemm_precision in ("f32", "f32split")
     K = 35 if args.attack == "ultrasonic" else 10
-    waves, labels = synth.make_clips_torch(args.n_train, cfg.sample_rate, cfg.length, K, seed=35 + rank, device=dev)
+    n_clips = args.n_train * world
+    waves, labels = synth.make_clips_torch(n_clips, cfg.sample_rate, cfg.length, K, seed=35, device=dev)
     if cfg.clean_label:  # FlowMur poisons target-class clips only: make sure there are some
-        labels[: args.n_train // 4] = cfg.target_label
+        labels[: n_clips // 4] = cfg.target_label
     trigger = None
     if args.attack == "ultrasonic":
         trigger = ultrasonic_trigger(60, "mid", False)
@@ -195,7 +245,7 @@ def main():
     model = smallcnn(K, cfg.linear_features).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     tr = ResidentTrainer(cfg, waves, labels, model, opt, args.batch, trigger=trigger, seed=35, rank=rank,
-                         world=world, overlap_features=args.overlap, gemm_precision=args.gemm_precision)
+                         world=world, gemm_precision=args.gemm_precision, sync_bn=args.sync_bn)
 
     # warmup (untimed), then a few more untimed steps with every libabd phase bracketed to
     # find the dominant kernel in steady state
@@ -208,20 +258,33 @@ def main():
         torch.cuda.synchronize()
     phases_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in wprof.result.items()}
     dominant = max(wprof.result, key=lambda k: wprof.result[k][0]) if wprof.result else "conv2_dgrad"
+    # the feature stage is measured as a unit (SURVEY §8d bytes: wave in, MFCC out)
+    live = list(FEATURE_PHASES) if dominant in FEATURE_PHASES else [dominant]
 
-    prof = L.PhaseProfiler([dominant], max_records=args.steps + 4)
+    # timed region: exactly `steps` steps between barrier + synchronize; HIP events bracket the
+    # dominant kernel(s) on their launch stream, plus one event per window boundary
+    prof = L.PhaseProfiler(live, max_records=len(live) * args.steps + 8)
+    nwin = max(1, min(args.windows, args.steps))
+    bounds = [round(i * args.steps / nwin) for i in range(nwin + 1)]
+    wev = [torch.cuda.Event(enable_timing=True) for _ in bounds]
     prof.__enter__()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    wev[0].record()
+    bi = 1
+    for k in range(args.steps):
         tr.step()
+        if bi < len(bounds) and k + 1 == bounds[bi]:
+            wev[bi].record()
+            bi += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     prof.__exit__(None, None, None)
+    win_ms = [wev[i].elapsed_time(wev[i + 1]) / max(bounds[i + 1] - bounds[i], 1) for i in range(nwin)]
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -229,19 +292,46 @@ def main():
     metrics = tr.read_metrics()
 
     if rank == 0:
+        import statistics
         n_utt = args.batch * world * args.steps
-        ms, cnt = prof.result.get(dominant, (0.0, 0))
-        avg_s = ms / max(cnt, 1) / 1e3
         T, C, L_ = tr.T, cfg.n_mfcc, cfg.length
-        work = algorithmic_work(dominant, args.batch, T, C, K, 128, T, C, L_)
         roof = None
-        if work is not None and avg_s > 0:
-            amount, unit, bound = work
+        ms_live = {ph: prof.result.get(ph, (0.0, 0)) for ph in live}
+        cnt = min(c for _, c in ms_live.values()) if ms_live else 0
+        avg_s = sum(ms / max(c, 1) for ms, c in ms_live.values()) / 1e3
+        if cnt > 0 and avg_s > 0:
+            if dominant in FEATURE_PHASES:
+                amount = args.batch * feature_bytes(L_, T, C) / 1e9
+                unit, bound, peak = "GB/s", "hbm", HBM_PEAK_GBPS
+                traffic = None
+                if headline:
+                    tb = [load_traffic(ph) for ph in live]
+                    traffic = sum(tb) if all(v is not None for v in tb) else None
+            else:
+                amount, unit, bound = algorithmic_work(dominant, args.batch, T, C, K, 128, T, C, L_)
+                peak = mfma_peak(dominant) if bound == "mfma" else HBM_PEAK_GBPS
+                traffic = load_traffic(dominant) if headline else None
             achieved = amount / avg_s
-            peak = mfma_peak(dominant) if bound == "mfma" else HBM_PEAK_GBPS
-            roof = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                    "frac": round(achieved / peak, 4), "traffic": load_traffic(dominant) if headline else None,
-                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt}
+            roof = {"kernel": "+".join(live), "bound": bound, "achieved": round(achieved, 3), "peak": peak,
+                    "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "algorithmic_bytes": round(amount * 1e9) if unit == "GB/s" else None,
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
+                    "formula": ("B*(4L + 4*T*C) / (avg stft_mel + avg db_dct) [SURVEY 8d feature bytes]"
+                                if dominant in FEATURE_PHASES else "per-launch algorithmic FLOP / avg launch")}
+            if dominant == "stft_mel" and args.attack == "ultrasonic":
+                st_ms, st_c = ms_live["stft_mel"]
+                roof["note"] = ("HBM-bound by the survey's byte model but VALU-limited in practice: "
+                                f"{stft_flops(args.batch, T) / (st_ms / st_c / 1e3) / 1e12:.1f} TFLOP/s of FFT "
+                                f"arithmetic in stft_mel (fp32 vector peak {FP32_MFMA_PEAK_TFLOPS})")
+        # step-level roofline: ideal time per utterance = feature bytes / HBM + train FLOPs / fp32 peak
+        H0, W0 = T, C
+        t_ideal = args.batch * (feature_bytes(L_, T, C) / (HBM_PEAK_GBPS * 1e9)
+                                + train_flops(H0, W0, K) / (FP32_MFMA_PEAK_TFLOPS * 1e12))
+        step_s = dt / args.steps
+        step_roof = {"t_ideal_ms": round(t_ideal * 1e3, 4), "t_step_ms": round(step_s * 1e3, 4),
+                     "frac": round(t_ideal / step_s, 4), "feature_bytes_per_utt": feature_bytes(L_, T, C),
+                     "train_flops_per_utt": train_flops(H0, W0, K),
+                     "peaks": f"HBM {HBM_PEAK_GBPS} GB/s, fp32 MFMA {FP32_MFMA_PEAK_TFLOPS} TFLOP/s"}
         # every phase with an algorithmic work model, from the untimed per-phase profiling steps
         per_kernel = {}
         for ph, (pms, pcnt) in wprof.result.items():
@@ -253,24 +343,22 @@ def main():
             pk = mfma_peak(ph) if bnd == "mfma" else HBM_PEAK_GBPS
             per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "frac": round(ach / pk, 4),
                               "ms": round(pms / pcnt, 4), "traffic": load_traffic(ph) if headline else None}
-        if roof is not None and dominant == "stft_mel" and args.attack == "ultrasonic":
-            # the STFT moves few bytes per FLOP: its real limit is VALU issue (FFT butterflies),
-            # reported beside the HBM fraction the metric asks for
-            roof["note"] = ("HBM-bound by the survey's byte model but VALU-limited in practice: "
-                            f"{stft_flops(args.batch, T) / avg_s / 1e12:.1f} TFLOP/s of FFT arithmetic "
-                            f"(fp32 vector peak {FP32_MFMA_PEAK_TFLOPS})")
         cpu = None
-        if world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.attack == "ultrasonic":
-            threads = min(16, len(os.sched_getaffinity(0)))
-            cpu = cpu_baseline(args.cpu_sample, threads)
+        if world == 1 and not args.no_cpu and args.cpu_steps > 0 and args.attack == "ultrasonic":
+            cpu = cpu_baseline(args.batch, cpu_threads(), args.cpu_steps)
+        value = n_utt / dt
         line = {
             "metric": "poisoned+clean utterances/sec/GPU; ASR & clean-acc parity vs reference",
-            "value": round(n_utt / dt, 1),
+            "value": round(value, 1),
             "unit": "utterances/s",
+            "value_semantics": "whole-job utterances/s over all ranks (per-GPU figure in value_per_gpu)",
+            "value_per_gpu": round(value / world, 1),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step_window_median": round(statistics.median(win_ms), 4),
+            "ms_per_step_windows": [round(v, 4) for v in win_ms],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -280,8 +368,9 @@ def main():
             "config": {"workload": WORKLOADS[args.attack], "attack": args.attack, "num_classes": K,
                        "gemm_precision": args.gemm_precision, "per_gpu_batch": args.batch,
                        "global_batch": args.batch * world, "poisoning_rate": cfg.poisoning_rate,
-                       "resident_clips_per_gpu": args.n_train, "parallelism": f"dp{world}"},
+                       "resident_clips": n_clips, "sync_bn": bool(args.sync_bn), "parallelism": f"dp{world}"},
             "roofline": roof,
+            "step_roofline": step_roof,
             "cpu_baseline": cpu,
             "phases_ms_per_launch": phases_ms,
             "roofline_by_kernel": per_kernel,

@@ -264,7 +264,24 @@ typedef struct abd_train_args {
                               * abd_smallcnn_param_offsets()[12]) are final, so
                               * a DP caller can start their all-reduce while the
                               * conv backward is still running               */
+  int64_t row_offset;        /* DP: global batch row of this rank's row 0.  The
+                              * generated dropout masks hash the GLOBAL element
+                              * index, so N ranks on slices of one global batch
+                              * draw exactly the masks one process would.     */
+  /* Synchronised BatchNorm (optional; NULL = per-rank statistics like DDP).  At each of the
+   * 6 BatchNorm reductions of a step (forward bn1..bn3, then backward bn3..bn1) libabd writes
+   * this rank's per-channel double sums into bn_sync_buf + point * ABD_BN_SYNC_STRIDE
+   * (2*C+1 doubles: [sum_c | sum2_c | element count] forward, [sum dy_c | sum dy*xhat_c | count]
+   * backward) and calls bn_sync(ctx, point, offset, n) from the launching thread; the callback
+   * must enqueue an in-place SUM all-reduce of those n doubles on `stream` (torch.distributed
+   * on the current stream does).  The statistics then use the global sums and counts: the
+   * normalisation, running statistics and input gradients equal one process's on the global
+   * batch; BN weight/bias gradients stay this rank's share (summed by the gradient all-reduce). */
+  double* bn_sync_buf;       /* device, >= 6 * ABD_BN_SYNC_STRIDE doubles               */
+  int (*bn_sync)(void* ctx, int point, int64_t offset, int64_t n);
+  void* bn_sync_ctx;
 } abd_train_args;
+#define ABD_BN_SYNC_STRIDE 136
 
 int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspace,
                             size_t workspace_bytes, abd_stream_t stream);

@@ -26,3 +26,9 @@ def golden():
 def wavs():
     import numpy as np
     return dict(np.load(os.path.join(GOLDEN, "ultrasonic_wavs.npz")))
+
+
+@pytest.fixture(scope="session")
+def conv_golden():
+    import numpy as np
+    return dict(np.load(os.path.join(GOLDEN, "convergence_ref.npz")))

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Multi-epoch convergence fixtures from the REFERENCE's own training loop.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/make_convergence.py [badnets|ultrasonic ...]
+
+For each config in tests/golden_inputs.CONV_CFGS this follows eval_model (badnets.py:127-160;
+ultrasonic.py:155-188) with the reference's modules: ``utils.models.smallcnn`` built under a fixed
+torch seed (the reference builds it before fix_random, so its init is otherwise unseeded),
+``torch.optim.Adam(lr=1e-4)``, ``nn.CrossEntropyLoss``, ``utils.random_tools.fix_random()``, the
+poisoned data of badnets_poison_data / ultrasonic_poison_data (tests/golden_inputs.convergence_data),
+shuffled DataLoaders of the reference's batch size, then per epoch ``utils.training_tools.train``
+and ``test``.  Stored: per-epoch train() / test() results, digests of the final state_dict, and a
+digest of the input features (so a replay on another host can prove it fed identical inputs).
+
+The dropout masks are not stored: the reference's CPU forward draws them from the global CPU
+generator with bernoulli_(1 - p) (ATen's non-fused CPU dropout), and the replay redraws them the
+same way (abd_amd.models.torch_cpu_masks) -- checked here against masks captured by hooks.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+
+REF = os.environ.get("ABD_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from golden_inputs import CONV_CFGS, convergence_data, data_digest  # noqa: E402
+
+import utils.models as ref_models  # noqa: E402
+import utils.training_tools as ref_tt  # noqa: E402
+import utils.random_tools as ref_rt  # noqa: E402
+
+
+class DictSet(torch.utils.data.Dataset):
+    """The reference BDDataset item contract (prepare_dataset.py:13-33)."""
+
+    def __init__(self, x, y, ind):
+        self.x, self.y, self.ind = x, y, ind
+
+    def __len__(self):
+        return len(self.x)
+
+    def __getitem__(self, i):
+        return {"mfcc": self.x[i], "label": self.y[i], "poison_indicator": self.ind[i]}
+
+
+def digest(t: np.ndarray, seed: int, n=64):
+    t = np.asarray(t, dtype=np.float64).reshape(-1)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    idx = rng.choice(t.size, size=min(n, t.size), replace=False)
+    return np.concatenate([[t.sum(), np.sqrt((t * t).sum())], t[idx]])
+
+
+def run(name, out):
+    c = CONV_CFGS[name]
+    torch.manual_seed(c["init_seed"])
+    m = ref_models.smallcnn(c["K"], c["lf"])                       # badnets.py:128 (before fix_random)
+    crit = torch.nn.CrossEntropyLoss()                             # :132
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)                # :133
+    ref_rt.fix_random()                                            # :134
+    d = convergence_data(name)                                     # :137 (badnets_poison_data)
+    B = c["B"]
+    clean = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(torch.tensor(d["clean_x"]),
+                                                                       torch.tensor(d["clean_y"])),
+                                        batch_size=B, shuffle=True)
+    bd_train = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bd_x"]), torch.tensor(d["bd_y"]),
+                                                   torch.tensor(d["ind"])), batch_size=B, shuffle=True)
+    bd_test = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bt_x"]), torch.tensor(d["bt_y"]),
+                                                  torch.tensor(d["bt_ind"])), batch_size=B, shuffle=True)
+    # pin the mask redraw recipe on the first batch: hook-captured masks == bernoulli_ redraw
+    captured = []
+
+    def hook(mod, inp, o):
+        if mod.training and len(captured) < 2:
+            captured.append(((o.detach() != 0).reshape(o.shape[0], -1), (inp[0].detach() != 0).reshape(o.shape[0], -1)))
+    hs = [m.drop1.register_forward_hook(hook), m.drop2.register_forward_hook(hook)]
+    state = torch.get_rng_state()
+    tr, te = [], []
+    t0 = time.time()
+    for epoch in range(c["epochs"]):
+        tr.append(ref_tt.train(m, bd_train, torch.device("cpu"), opt, crit))
+        if epoch == 0:
+            for h in hs:
+                h.remove()
+        te.append(ref_tt.test(m, torch.device("cpu"), clean, bd_test, crit))
+        print(f"{name} epoch {epoch + 1}: train {tr[-1]}  test {te[-1]}  ({time.time() - t0:.0f} s)", flush=True)
+    # redraw: base seed + sampler seed (DataLoader iter), then drop1, drop2 of batch 0
+    torch.set_rng_state(state)
+    torch.empty((), dtype=torch.int64).random_()
+    torch.empty((), dtype=torch.int64).random_()
+    flat = c["lf"]
+    m1 = torch.empty((B, flat)).bernoulli_(0.6).bool()
+    m2 = torch.empty((B, 128)).bernoulli_(0.5).bool()
+    for mine, (kept, live) in ((m1, captured[0]), (m2, captured[1])):   # decidable where the input is non-zero
+        assert torch.equal(mine[live], kept[live]), "mask redraw recipe drifted"
+    out[f"{name}_train"] = np.array(tr, dtype=np.float64)
+    out[f"{name}_test"] = np.array(te, dtype=np.float64)
+    out[f"{name}_data_digest"] = data_digest(d)
+    for k, v in m.state_dict().items():
+        out[f"{name}_final_{k}"] = digest(v.numpy(), 21)
+
+
+def main():
+    names = sys.argv[1:] or list(CONV_CFGS)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    path = os.path.join(HERE, "convergence_ref.npz")
+    out = dict(np.load(path)) if os.path.exists(path) else {}
+    for n in names:
+        run(n, out)
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()

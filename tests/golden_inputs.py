@@ -128,5 +128,80 @@ def flowmur_inputs(seed=91):
     return waves, pos, labels, state
 
 
+# Multi-epoch convergence fixtures (tests/golden/make_convergence.py): the reference's own
+# eval_model loop (badnets.py:127-160 / ultrasonic.py:155-188: model built, fix_random(), poisoned
+# data, shuffled loaders, train() + test() per epoch) on synthetic class-conditional clips.
+CONV_CFGS = {
+    "badnets": dict(attack="badnets", sr=16000, L=16000, n_fft=400, hop=160, n_mfcc=40, K=10, lf=3072, B=256,
+                    n_train=2048, n_test=512, epochs=8, clip_seed=101, init_seed=1234),
+    "ultrasonic": dict(attack="ultrasonic", sr=44100, L=44100, n_fft=1103, hop=441, n_mfcc=40, K=35, lf=3072,
+                       B=512, n_train=4096, n_test=1024, epochs=14, clip_seed=102, init_seed=1235),
+}
+
+
+def ultrasonic_trigger_f32():
+    """GenerateTrigger(60, 'mid', cont=False).trigger() (ultrasonic.py:41-42 defaults, utils/ultra_trigger.py)
+    on the packaged trigger.wav samples, as float32 (torchaudio.load's dtype)."""
+    import os
+    from oracle.triggers import ultrasonic_gate
+    here = os.path.dirname(os.path.abspath(__file__))
+    t = np.load(os.path.join(here, "golden", "ultrasonic_wavs.npz"))["ultrasonic_trigger_int16"]
+    return ultrasonic_gate(t[None].astype(np.float64) / 32768.0, 60, "mid", cont=False).astype(np.float32)
+
+
+def convergence_data(name):
+    """Clean / poisoned features exactly as badnets_poison_data (badnets.py:38-95) or
+    ultrasonic_poison_data (ultrasonic.py:40-124) builds them, from deterministic synthetic clips.
+
+    Must run right after fix_random() (it draws the poisoned rows with the global ``random``).
+    Features come from oracle.torch_ref.mfcc, the torch-CPU restatement of torchaudio's T.MFCC."""
+    import random
+
+    import torch
+    from abd_amd import synth
+    from oracle import torch_ref
+    c = CONV_CFGS[name]
+    n = c["n_train"] + c["n_test"]
+    waves, labels = synth.make_clips_np(n, c["sr"], c["L"], c["K"], seed=c["clip_seed"])
+
+    def feats(w):
+        return torch_ref.mfcc(torch.from_numpy(np.ascontiguousarray(w)), c["sr"], c["n_mfcc"], c["n_fft"],
+                              c["hop"]).numpy()
+
+    clean = feats(waves)
+    ntr = c["n_train"]
+    tr_x, te_x = clean[:ntr].copy(), clean[ntr:].copy()
+    tr_y, te_y = labels[:ntr].copy(), labels[ntr:].copy()
+    T, C = tr_x.shape[2], tr_x.shape[3]
+    rows = random.sample(list(range(ntr)), int(ntr * 0.1))      # badnets.py:50-51 / ultrasonic.py:70-71
+    ind = np.zeros(ntr, np.int64)
+    ind[rows] = 1
+    bd_y = tr_y.copy()
+    bd_y[rows] = 2
+    test_pois = te_y != 2
+    if c["attack"] == "badnets":
+        def poison(x):
+            x[:, :, T - 5:T, C - 5:C] = -200.0   # generate_trigger(W, H, 5) + add_trigger_to_mfcc
+            return x
+        bd_x = tr_x.copy()
+        bd_x[rows] = poison(bd_x[rows])
+        bt_x = te_x.copy()
+        bt_x[test_pois] = poison(bt_x[test_pois])
+    else:
+        trig = ultrasonic_trigger_f32()
+        bd_x = tr_x.copy()
+        srt = np.sort(rows)
+        bd_x[srt] = feats(waves[:ntr][srt] + trig)
+        bt_x = te_x.copy()
+        bt_x[test_pois] = feats(waves[ntr:][test_pois] + trig)
+    return dict(bd_x=bd_x, bd_y=bd_y.astype(np.int64), ind=ind, clean_x=te_x, clean_y=te_y.astype(np.int64),
+                bt_x=bt_x, bt_y=np.full(c["n_test"], 2, np.int64), bt_ind=test_pois.astype(np.int64))
+
+
+def data_digest(d):
+    return np.array([float(np.asarray(d[k], np.float64).sum()) for k in sorted(d)] +
+                    [float(np.abs(np.asarray(d[k], np.float64)).sum()) for k in sorted(d)])
+
+
 def unpack_mask(packed, n_cols):
     return np.unpackbits(packed, axis=-1)[..., :n_cols].astype(np.float64)

@@ -1,0 +1,129 @@
+"""GPU: multi-epoch convergence parity with the reference's own eval_model loop.
+
+tests/golden/make_convergence.py ran the reference's ``utils.models.smallcnn`` +
+``utils.training_tools.train/test`` for several epochs on poisoned features (badnets.py:127-160,
+ultrasonic.py:155-188 at B = 512, K = 35).  Here the same loop runs through the drop-in surface
+(``abd_amd.training.train/test`` -- what ``dropin/utils/training_tools`` exports -- with the abd
+``smallcnn`` on the MI355X) on identical inputs:
+
+* replay: ``dropout_source='torch_cpu'`` draws every dropout mask exactly as the reference's CPU
+  forward does, so the whole run consumes the CPU RNG stream like the reference (same masks, same
+  shuffled batch orders).  Per-epoch train loss / test losses within 1e-4 relative (north_star),
+  accuracies and ASR equal.
+* device dropout: the production path (masks from the device hash).  Final clean accuracy and ASR
+  within +-0.5 pp of the reference's (north_star target).
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import abd_amd
+from abd_amd import training as T
+from abd_amd.models import smallcnn
+from golden_inputs import CONV_CFGS, convergence_data, data_digest
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    abd_amd.load_library()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def conv_ref():
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "convergence_ref.npz")
+    return dict(np.load(p))
+
+
+class DictSet(torch.utils.data.Dataset):
+    def __init__(self, x, y, ind):
+        self.x, self.y, self.ind = x, y, ind
+
+    def __len__(self):
+        return len(self.x)
+
+    def __getitem__(self, i):
+        return {"mfcc": self.x[i], "label": self.y[i], "poison_indicator": self.ind[i]}
+
+
+def fix_random(seed=35):
+    """utils/random_tools.py:5-18"""
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+
+
+_DATA = {}
+
+
+def eval_model(name, dev, source, ref):
+    c = CONV_CFGS[name]
+    torch.manual_seed(c["init_seed"])
+    m = smallcnn(c["K"], c["lf"])
+    m.to(dev)
+    crit = torch.nn.CrossEntropyLoss()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    fix_random()
+    if name not in _DATA:      # deterministic after fix_random(): built once per module
+        _DATA[name] = convergence_data(name)
+    d = _DATA[name]
+    dg, rdg = data_digest(d), ref[f"{name}_data_digest"]
+    assert np.allclose(dg, rdg, rtol=1e-6, atol=0), ("host features differ from the fixture's", dg - rdg)
+    B = c["B"]
+    clean = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(torch.tensor(d["clean_x"]),
+                                                                       torch.tensor(d["clean_y"])),
+                                        batch_size=B, shuffle=True)
+    bd_train = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bd_x"]), torch.tensor(d["bd_y"]),
+                                                   torch.tensor(d["ind"])), batch_size=B, shuffle=True)
+    bd_test = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bt_x"]), torch.tensor(d["bt_y"]),
+                                                  torch.tensor(d["bt_ind"])), batch_size=B, shuffle=True)
+    m.set_dropout_source(source)
+    tr, te = [], []
+    for _ in range(c["epochs"]):
+        tr.append(T.train(m, bd_train, dev, opt, crit))
+        te.append(T.test(m, dev, clean, bd_test, crit))
+    return np.array(tr), np.array(te), m
+
+
+@pytest.mark.parametrize("name", list(CONV_CFGS))
+def test_replay_matches_reference_epochs(dev, conv_ref, name):
+    tr, te, m = eval_model(name, dev, "torch_cpu", conv_ref)
+    rtr, rte = conv_ref[f"{name}_train"], conv_ref[f"{name}_test"]
+    n_train, n_test = CONV_CFGS[name]["n_train"], CONV_CFGS[name]["n_test"]
+    for e in range(len(rtr)):
+        assert tr[e, 0] == pytest.approx(rtr[e, 0], rel=RTOL), ("train loss", e, tr[e], rtr[e])
+        # accuracies are counts / n: equal counts <=> equal percentages
+        assert round(tr[e, 1] * n_train / 100) == round(rtr[e, 1] * n_train / 100), ("mix acc", e, tr[e], rtr[e])
+        assert tr[e, 2] == pytest.approx(rtr[e, 2]), ("train asr", e, tr[e], rtr[e])
+        assert round(te[e, 0] * n_test / 100) == round(rte[e, 0] * n_test / 100), ("clean acc", e, te[e], rte[e])
+        assert te[e, 1] == pytest.approx(rte[e, 1]), ("test asr", e, te[e], rte[e])
+        # test losses: means of small per-sample losses (log-probs near 0) -- absolute floor of
+        # a few fp32 ulps of the logits
+        assert te[e, 2] == pytest.approx(rte[e, 2], rel=RTOL, abs=2e-6), ("clean loss", e, te[e], rte[e])
+        assert te[e, 3] == pytest.approx(rte[e, 3], rel=RTOL, abs=2e-6), ("bd loss", e, te[e], rte[e])
+    from test_oracle_golden import _digest
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    for k, v in sd.items():
+        if k.endswith("num_batches_tracked"):
+            continue
+        ref = conv_ref[f"{name}_final_{k}"]
+        mine = _digest(v, 21)
+        assert abs(mine[1] - ref[1]) <= 1e-3 * abs(ref[1]), k
+        assert np.abs(mine[2:] - ref[2:]).max() <= 1e-2 * np.abs(ref[2:]).max(), k
+
+
+@pytest.mark.parametrize("name", list(CONV_CFGS))
+def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name):
+    tr, te, _ = eval_model(name, dev, "device", conv_ref)
+    rte = conv_ref[f"{name}_test"]
+    assert tr[-1, 0] < tr[0, 0]                                  # training converges
+    assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5, (te[-1], rte[-1])   # clean accuracy (pp)
+    assert abs(te[-1, 1] - rte[-1, 1]) <= 0.5, (te[-1], rte[-1])   # attack success rate (pp)

@@ -99,3 +99,80 @@ def test_overlapped_allreduce_matches_gathered_sum():
         assert tb is None, tb
         assert max(errs) < 1e-6, errs          # overlapped buckets == sum of the shards' gradients
         assert same == 0.0                     # identical Adam updates on every rank
+
+
+def _equiv_worker(rank, world, port, q):
+    """2 ranks x B/2 with synchronised BatchNorm vs 1 rank x B, same global batches."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import torch.distributed as dist
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import abd_amd
+        from abd_amd import synth, training as T
+        from abd_amd.models import smallcnn
+        from abd_amd.pipeline import ResidentTrainer, attack_config
+        abd_amd.load_library()
+        cfg = attack_config("badnets")
+        B, K, steps = 64, 10, 3
+        waves, labels = synth.make_clips_torch(256, cfg.sample_rate, cfg.length, K, seed=35, device=dev)
+
+        def run(world_, rank_, pg_world):
+            torch.manual_seed(35)
+            model = smallcnn(K, cfg.linear_features).to(dev)
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+            tr = ResidentTrainer(cfg, waves, labels, model, opt, B // world_, seed=35, rank=rank_, world=world_,
+                                 sync_bn=world_ > 1)
+            for _ in range(steps):
+                tr.step()
+            m = tr.read_metrics()
+            eng = model._engine
+            torch.cuda.synchronize()
+            return eng.params.clone(), eng.running.clone(), m, tr
+
+        p2, r2, m2, tr2 = run(world, rank, world)
+        assert tr2.bn_sync is not None and tr2.bn_sync.calls == 6 * steps, tr2.bn_sync.calls
+        # dropout masks of the two ranks hash their GLOBAL rows: rank 1 must not repeat rank 0's
+        eng = tr2.model._engine
+        x = torch.zeros((B // world, 1, tr2.T, cfg.n_mfcc), device=dev)
+        mo = (torch.empty((B // world, eng.flat), dtype=torch.uint8, device=dev),
+              torch.empty((B // world, 128), dtype=torch.uint8, device=dev))
+        T.train_step(tr2.model, x, torch.zeros(B // world, dtype=torch.int64, device=dev), None, None, None,
+                     masks_out=mo, do_update=False, seed=9, row_offset=rank * (B // world))
+        parts = [torch.zeros_like(mo[0]) for _ in range(world)]
+        dist.all_gather(parts, mo[0])
+        masks_differ = not torch.equal(parts[0], parts[1])
+        res = None
+        if rank == 0:
+            p1, r1, m1, _ = run(1, 0, 1)
+            nrel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+            res = {"params": nrel(p2, p1), "running": nrel(r2, r1), "loss": abs(m2["loss"] - m1["loss"]) / m1["loss"],
+                   "acc": (m2["acc"], m1["acc"]), "samples": (m2["samples"], m1["samples"])}
+        q.put((rank, res, masks_differ, None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+        raise
+
+
+def test_two_rank_sync_bn_step_equals_one_rank_step():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_equiv_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=110) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    for rank, r, differ, tb in res:
+        assert tb is None, tb
+        assert differ, "ranks drew identical dropout masks"
+        if rank == 0:
+            assert r["params"] < 1e-5 and r["running"] < 1e-5, r
+            assert r["loss"] < 1e-5 and r["acc"][0] == r["acc"][1] and r["samples"][0] == r["samples"][1], r
