@@ -44,7 +44,10 @@ def prepare_clean_dataset(data_path, directory_name, labels, waveform_to_conside
             if rate != sr:  # only ultrasonic changes rate (16 kHz -> 44.1 kHz)
                 w = resample(torch.from_numpy(w), rate, sr).numpy()
             if w.shape[0] >= waveform_to_consider:
-                waves.append(w[None, :waveform_to_consider])
+                # prepare_dataset.py:61-63: `waveform[:waveform_to_consider]` slices the CHANNEL dim of
+                # the (1, L) tensor, so every kept clip is kept whole; clips of different lengths make
+                # the reference's np.array() fail, and np.stack fails here the same way
+                waves.append(w[None, :])
                 labs.append(li)
     waves = np.stack(waves).astype(np.float32)
     dev = torch.device("cuda", torch.cuda.current_device())

