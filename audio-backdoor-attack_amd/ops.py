@@ -4,6 +4,7 @@
     torch.ops.abd.mfcc                 prepare_dataset.py:35-47 (+ the fused trigger injection)
     torch.ops.abd.inject_waveform      ultrasonic.py:75, flowmur.py:77-85 / 101-106
     torch.ops.abd.smallcnn_eval        utils/models.py:43-65 in eval mode
+    torch.ops.abd.smallcnn_eval_metrics  the same + test()'s counters (utils/training_tools.py:98-128)
     torch.ops.abd.smallcnn_train_step  utils/training_tools.py:60-79: forward, CE, backward, Adam,
                                        loss / accuracy / ASR counters -- one launch sequence
     torch.ops.abd.adam                 torch.optim.Adam single-tensor step (flat buffers)
@@ -97,26 +98,39 @@ def _(waves, trigger, mode, poison=None, position=None, snr_db=30.0):
 
 
 # --------------------------------------------------------------------------- smallcnn
-@torch.library.custom_op("abd::smallcnn_eval", mutates_args=("metrics",))
-def smallcnn_eval(x: Tensor, params: Tensor, running: Tensor, num_classes: int, precision: str = "f32",
-                  labels: Optional[Tensor] = None, indicators: Optional[Tensor] = None,
-                  metrics: Optional[Tensor] = None) -> Tensor:
-    """model.eval() forward: (B, 1, H0, W0) -> log-probs (B, K); running BN statistics, no dropout.
-    With labels + metrics (int64[8]) it also accumulates test()'s loss / accuracy / ASR counters
-    (utils/training_tools.py:98-128)."""
+def _eval(x, params, running, num_classes, precision, labels, indicators, metrics):
     L.require_device(x, "smallcnn input")
     B, H0, W0 = int(x.shape[0]), int(x.shape[2]), int(x.shape[3])
     h = _net(H0, W0, num_classes, precision)
     out = torch.empty((B, int(num_classes)), dtype=torch.float32, device=x.device)
     ws = _ws(L.lib().abd_smallcnn_workspace_bytes(h, B), x.device)
     L.check(L.lib().abd_smallcnn_eval(h, x.data_ptr(), B, params.data_ptr(), running.data_ptr(), _ptr(labels),
-                                      _ptr(indicators), out.data_ptr(), _ptr(metrics) if labels is not None else None,
-                                      ws.data_ptr(), ws.numel(), L.stream_ptr(x.device)), "abd_smallcnn_eval")
+                                      _ptr(indicators), out.data_ptr(), _ptr(metrics), ws.data_ptr(), ws.numel(),
+                                      L.stream_ptr(x.device)), "abd_smallcnn_eval")
     return out
 
 
+@torch.library.custom_op("abd::smallcnn_eval", mutates_args=())
+def smallcnn_eval(x: Tensor, params: Tensor, running: Tensor, num_classes: int, precision: str = "f32") -> Tensor:
+    """model.eval() forward: (B, 1, H0, W0) -> log-probs (B, K); running BN statistics, no dropout."""
+    return _eval(x, params, running, num_classes, precision, None, None, None)
+
+
 @smallcnn_eval.register_fake
-def _(x, params, running, num_classes, precision="f32", labels=None, indicators=None, metrics=None):
+def _(x, params, running, num_classes, precision="f32"):
+    return x.new_empty((x.shape[0], num_classes))
+
+
+@torch.library.custom_op("abd::smallcnn_eval_metrics", mutates_args=("metrics",))
+def smallcnn_eval_metrics(x: Tensor, params: Tensor, running: Tensor, num_classes: int, precision: str,
+                          labels: Tensor, indicators: Optional[Tensor], metrics: Tensor) -> Tensor:
+    """The eval forward plus test()'s loss / accuracy / ASR counters accumulated into metrics
+    (int64[8]; utils/training_tools.py:98-128); returns the log-probs."""
+    return _eval(x, params, running, num_classes, precision, labels, indicators, metrics)
+
+
+@smallcnn_eval_metrics.register_fake
+def _(x, params, running, num_classes, precision, labels, indicators, metrics):
     return x.new_empty((x.shape[0], num_classes))
 
 

@@ -199,7 +199,8 @@ def _eval_batches(model, loader, dev, dict_items):
         y = _as_long(y, dev)
         ind = _as_long(ind, dev) if ind is not None else None
         eng = model.engine(x)
-        torch.ops.abd.smallcnn_eval(x, eng.params, eng.running, eng.K, model.gemm_precision, y, ind, metrics)
+        torch.ops.abd.smallcnn_eval_metrics(x, eng.params, eng.running, eng.K, model.gemm_precision, y, ind,
+                                            metrics)
         n += 1
     return read_metrics(metrics), n
 

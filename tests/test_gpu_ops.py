@@ -68,8 +68,10 @@ def test_opcheck_smallcnn_eval(dev):
         assert torch.equal(y, m(x))   # the module's eval forward is this op
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     labels = torch.tensor([0, 1, 2, 3], device=dev)
-    torch.library.opcheck(torch.ops.abd.smallcnn_eval.default, (x, eng.params, eng.running, 10),
-                          dict(labels=labels, metrics=metrics))
+    torch.library.opcheck(torch.ops.abd.smallcnn_eval_metrics.default,
+                          (x, eng.params, eng.running, 10, "f32", labels, None, metrics))
+    y2 = torch.ops.abd.smallcnn_eval_metrics(x, eng.params, eng.running, 10, "f32", labels, None, metrics)
+    assert torch.equal(y2, y) and int(metrics[1]) > 0
 
 
 def test_opcheck_smallcnn_train_step_and_adam(dev):
