@@ -936,8 +936,19 @@ __device__ __forceinline__ void load_item(float2* buf, const float* x, const Mfc
 //   -> in-place power |A_k|^2, |B_k|^2 (Bluestein output chirp fused)
 //   -> mel by half-filter slots (2 per filter, balanced), halves combined by a lane swap
 //   -> 10 log10 -> ws_db, per-item max -> ws_max.
+// ABD_TW_LDS: stage the inter-pass twiddle tables (4 KB) in LDS.  Off by default: read through
+// the L1 instead, the Bluestein block's LDS drops from 23.7 to 19.6 KB and 8 blocks (32 waves, the
+// CU maximum) fit instead of 6 -- the kernel is latency-bound (46 % of wave cycles parked at
+// barriers / waitcnt, profiles/r2_stft_pmc.txt), so the extra residency is what pays.
+#ifdef ABD_TW_LDS
+constexpr bool kTwLds = true;
+#else
+constexpr bool kTwLds = false;
+#endif
+constexpr int kBlueBlocks = kTwLds ? 6 : 8;
+
 template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
-__global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
+__global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
                                                                  int64_t row_stride,
                                                                  const int32_t* __restrict__ rows, int64_t batch,
                                                                  InjDev inj, const float* __restrict__ rowscale,
@@ -948,15 +959,17 @@ __global__ void __launch_bounds__(kThreads, BLUE ? 6 : 1) stft_mel_fast_kernel(M
   // first FFT's first pass reads rows r < ceil(N / (M/R0)) only: the rest is never stored
   constexpr int kNZW = (BLUE && PP == 1) ? ((NN + M / R0 - 1) / (M / R0)) * (M / R0) : M;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  float2* tw = lds;
-  float2* buf = lds + NT;
+  constexpr int NTL = kTwLds ? NT : 0;
+  float2* buf = lds + NTL;
 #ifdef ABD_MEL_W_LDS
-  float* wl = reinterpret_cast<float*>(lds + NT + PP * (M + M / 16));
+  float* wl = reinterpret_cast<float*>(lds + NTL + PP * (M + M / 16));
 #else
-  const float* wl = p.mel2_w;  // 4-5 KB, L1-resident: keeps LDS at 6 blocks/CU
+  const float* wl = p.mel2_w;  // 4-5 KB, L1-resident: keeps the block's LDS to its FFT buffer
 #endif
   __shared__ float red[kThreads / kWave];
-  for (int i = ltid(); i < NT; i += kThreads) tw[i] = p.ftw[i];
+  const float2* tw = kTwLds ? lds : p.ftw;
+  if constexpr (kTwLds)
+    for (int i = ltid(); i < NT; i += kThreads) lds[i] = p.ftw[i];
 #ifdef ABD_MEL_W_LDS
   for (int i = ltid(); i < p.mel2_total; i += kThreads) wl[i] = p.mel2_w[i];
 #endif
@@ -1369,7 +1382,7 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
                 hipStream_t s) {
   auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE>;
   static_assert(M % 16 == 0, "padded LDS layout needs M % 16 == 0");
-  size_t lds = (size_t)(2 * R0 * R1 + PP * (M + M / 16)) * sizeof(float2);
+  size_t lds = (size_t)((kTwLds ? 2 * R0 * R1 : 0) + PP * (M + M / 16)) * sizeof(float2);
 #ifdef ABD_MEL_W_LDS
   lds += (size_t)((d.mel2_total + 3) & ~3) * 4;
 #endif

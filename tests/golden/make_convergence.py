@@ -117,21 +117,27 @@ SPREAD_THREADS = 3
 def main():
     """python make_convergence.py [names...]
 
-    Each config runs twice: with 8 intra-op threads (the fixture) and with SPREAD_THREADS threads,
-    stored as ``<name>_train_t3`` / ``<name>_test_t3``.  oneDNN's convolution and reduction orders
-    depend on the thread count, so the pair measures the reference's OWN fp32 run-to-run spread,
-    which over several epochs exceeds 1e-4 (chaotic amplification through Adam); the GPU replay
-    test is held to that envelope beyond its 1e-4 floor."""
+    Each config runs twice: the fixture (oneDNN convolutions, 8 intra-op threads) and a second fp32
+    implementation of the same loop -- ATen's native convolutions (oneDNN disabled) on
+    SPREAD_THREADS threads -- stored as ``<name>_train_alt`` / ``<name>_test_alt``.  The pair
+    measures the reference's OWN fp32 implementation-to-implementation spread (different summation
+    orders of the same math, which is exactly what a GPU kernel is), which over several epochs
+    exceeds 1e-4 (chaotic amplification through Adam); the GPU replay test is held to it."""
     names = sys.argv[1:] or list(CONV_CFGS)
     path = os.path.join(HERE, "convergence_ref.npz")
     out = dict(np.load(path)) if os.path.exists(path) else {}
+    only_alt = os.environ.get("ABD_ONLY_ALT") == "1"
     for n in names:
-        torch.set_num_threads(min(8, os.cpu_count() or 1))
-        run(n, out)
+        if not only_alt:
+            torch.set_num_threads(min(8, os.cpu_count() or 1))
+            run(n, out)
         torch.set_num_threads(SPREAD_THREADS)
-        spread = {}
-        run(n, spread)
-        out[f"{n}_train_t3"], out[f"{n}_test_t3"] = spread[f"{n}_train"], spread[f"{n}_test"]
+        alt = {}
+        with torch.backends.mkldnn.flags(enabled=False):
+            run(n, alt)
+        out[f"{n}_train_alt"], out[f"{n}_test_alt"] = alt[f"{n}_train"], alt[f"{n}_test"]
+        out.pop(f"{n}_train_t3", None)
+        out.pop(f"{n}_test_t3", None)
     np.savez_compressed(path, **out)
     print("wrote", path, len(out), "arrays")
 
