@@ -52,11 +52,16 @@ struct MfccDev {
   const int* mel_off;
   const float* mel_w;
   const float* dct;
+  const float4* dct_frag;  // db_dct_mfma_kernel B fragments: [s][q][tile][col] = dct[16s+4q+j][16 tile+col], j<4
+  int dct_tiles;           // ceil(n_mfcc / 16) when the MFMA DCT applies (n_mels % 16 == 0, n_mfcc <= 48), else 0
   // fast (specialised) kernel tables
   const float2* ftw;      // [W_{R0 R1}^e] ++ [W_M^k], e, k < R0 R1
+  const float2* ftw2;     // fast forward kernel: [k][r] tables W_{R0 R1}^{k r} (k < R0, r < R1) ++
+                          // W_M^{k r} (k < R0 R1, r < R2): every twiddle load is base + immediate
   const int4* mel2_meta;  // per half-filter slot 2m+h: (first bin, count, weight offset, 0)
   const float* mel2_w;    // compact slot weights
   int mel2_total, mel2_hp;  // #weights, max slot count rounded up to 8
+  const float* mel3_w;      // Bluestein fast path: kMelHP zero-padded weights per slot (NULL = unused)
   // backward (mel^T): the <= 2 filters that touch each bin (-1 = none) and their weights
   const int2* bin_mel;
   const float2* bin_w;
@@ -485,6 +490,74 @@ __global__ void __launch_bounds__(kThreads) db_dct_lds_kernel(MfccDev p, const f
   }
 }
 
+// dB clamp + DCT on the matrix cores: block = (utterance, 64 frames), wave = 16 frames x 16 NT
+// coefficients, v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation) over the mels.
+// Lane l feeds A[frame l & 15][mel] from one float4 of its frame's dB row per 16 mels (the K order
+// inside a 16-mel group is permuted identically in the host-built B fragments, MfccDev::dct_frag),
+// clamped at the utterance's top_db floor on the fly.  Replaces db_dct_lds_kernel, whose per-block
+// staging of the 20 KB DCT matrix and LDS float4 row reads bound it (36 us at B = 512, 100 frames).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <int NT>
+__global__ void __launch_bounds__(kThreads) db_dct_mfma_kernel(MfccDev p, const float* __restrict__ ws_db,
+                                                               const float* __restrict__ ws_max, InjDev inj,
+                                                               float* __restrict__ out) {
+  __shared__ float red[kThreads / kWave];
+  const int64_t u = blockIdx.x;
+  const int nv = inj.frames ? min(max(inj.frames[u], 0), p.T) : p.T;
+  float mx = -INFINITY;
+  if (nv < p.T) {
+    for (int i = threadIdx.x; i < nv * p.n_mels; i += kThreads) mx = fmaxf(mx, ws_db[u * p.T * p.n_mels + i]);
+  } else {
+    for (int i = threadIdx.x; i < p.chunks; i += kThreads) mx = fmaxf(mx, ws_max[u * p.chunks + i]);
+  }
+  mx = abd::wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x / kWave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float floor_db = (p.top_db >= 0.0f) ? mx - p.top_db : -INFINITY;
+  const int lane = threadIdx.x & 63;
+  const int t0 = (blockIdx.y * (kThreads / kWave) + (threadIdx.x >> 6)) * 16;
+  if (t0 >= p.T) return;
+  const int q = lane >> 4, col = lane & 15;
+  const float* arow = ws_db + ((int64_t)u * p.T + min(t0 + col, p.T - 1)) * p.n_mels + 4 * q;
+  const float4* bf = p.dct_frag + q * NT * 16 + col;
+  f32x4v acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const int ns = p.n_mels / 16;
+  for (int sg = 0; sg < ns; ++sg) {
+    float4 a = *reinterpret_cast<const float4*>(arow + 16 * sg);
+    a.x = fmaxf(a.x, floor_db);
+    a.y = fmaxf(a.y, floor_db);
+    a.z = fmaxf(a.z, floor_db);
+    a.w = fmaxf(a.w, floor_db);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const float4 b = bf[(sg * 4 * NT + n) * 16];
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[n], 0, 0, 0);
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[n], 0, 0, 0);
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[n], 0, 0, 0);
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[n], 0, 0, 0);
+    }
+  }
+  // D: lane holds frames t0 + 4q + i (i < 4) of coefficient 16 n + col
+  const bool pois = inj.patch && row_poisoned(inj, u);
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int c = 16 * n + col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + 4 * q + i;
+      if (t < p.T && c < p.n_mfcc) {
+        float v = acc[n][i];
+        if (pois && t >= inj.pt0 && t < inj.pt1 && c >= inj.pc0 && c < inj.pc1) v = inj.pval;
+        if (t >= nv) v = inj.fpad;
+        out[((int64_t)u * p.T + t) * p.n_mfcc + c] = v;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __restrict__ wave, int64_t row_stride,
                                                                int64_t L, const int32_t* __restrict__ rows,
                                                                InjDev inj, const float* __restrict__ rowscale,
@@ -561,10 +634,35 @@ constexpr f2v kPM = {1.0f, -1.0f};
 // t + (-i) d  and  t + i d
 __device__ __forceinline__ f2v add_mi(f2v t, f2v d) { return fmav(vswap(d), kPM, t); }
 __device__ __forceinline__ f2v add_pi(f2v t, f2v d) { return fmav(vswap(d), -kPM, t); }
-// a * w
+// a * w (compile-time w: the backend folds (-w.y, w.x) into an SGPR-pair literal, 2 instructions)
 __device__ __forceinline__ f2v cmulv(f2v a, f2v w) {
   const f2v ax = __builtin_shufflevector(a, a, 0, 0), ay = __builtin_shufflevector(a, a, 1, 1);
   return fmav(ay, __builtin_shufflevector(w, -w, 3, 0), ax * w);
+}
+// a * w and conj(a) * w for run-time w (table twiddles, chirps): the backend cannot fold the
+// one-sided negation into VOP3P modifiers and spends a v_pk_add + v_pk_mov building (-w.y, w.x)
+// (4 instructions); written out it is one v_pk_mul + one v_pk_fma with op_sel / neg modifiers:
+//   t = (a.x w.x, a.x w.y);  r.lo = -a.y w.y + t.lo,  r.hi = a.y w.x + t.hi   (conj: signs of a.y flip)
+__device__ __forceinline__ f2v cmul_rt(f2v a, f2v w) {
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+// value the compiler must treat as defined without materialising it (skip paths of the
+// wave-uniform pass guards: otherwise the backend zero-fills every register of the butterfly)
+__device__ __forceinline__ f2v undef_f2v() {
+  f2v v;
+  asm volatile("" : "=v"(v));
+  return v;
 }
 
 template <int R>
@@ -726,7 +824,7 @@ template <int R>
 __device__ __forceinline__ void tw_powers(f2v w1, f2v* w) {
   w[1] = w1;
 #pragma unroll
-  for (int r = 2; r < R; ++r) w[r] = (r % 2 == 0) ? cmulv(w[r / 2], w[r / 2]) : cmulv(w[r - 1], w1);
+  for (int r = 2; r < R; ++r) w[r] = (r % 2 == 0) ? cmul_rt(w[r / 2], w[r / 2]) : cmul_rt(w[r - 1], w1);
 }
 
 // One in-place Stockham pass over PP FFTs of length M: every thread reads its butterflies
@@ -734,10 +832,13 @@ __device__ __forceinline__ void tw_powers(f2v w1, f2v* w) {
 //   TWK 0: first pass (no twiddles)
 //   TWK 1: tw = W_{NS*R}^e table, factor W_{NS*R}^{k r} read directly (k < NS, r < R)
 //   TWK 2: tw = W_M^k table (k < NS, NS*R == M), factor (W_M^k)^r by tw_powers
+//   TWK 3: tw = [k][r] table of W_{NS*R}^{k r} (k < NS, r < R): one load per factor, no VALU
 //   VMUL : fold Bluestein's pointwise product conj(a) * vhat into the loads
 //   ZT   : rows r >= ZT are known zero (Bluestein's zero-padded input): not loaded, and the
 //          butterfly arithmetic on them folds away (mfcc.hip builds with -fno-signed-zeros)
-template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R>
+//   RS   : only rows r < RS of the output are stored (Bluestein's last pass: outputs >= N are
+//          never read; the arithmetic feeding only unstored rows is dead and folds away)
+template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R, int RS = R>
 __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* __restrict__ tws,
                                       const float2* __restrict__ vhats) {
   constexpr int MR = M / R;
@@ -770,15 +871,20 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
         }
         // MR % 16 == 0: pidx(rb + r MR) = pidx(rb) + r (MR + MR/16) -> base + immediate
         f2v a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
-        if constexpr (VMUL) a = cmulv(a * kPM, vhat[j + r * MR]);
+        if constexpr (VMUL) a = cmul_conj_rt(a, vhat[j + r * MR]);
         if constexpr (TWK == 1) {
-          if (r > 0) a = cmulv(a, tw[k * r]);
+          if (r > 0) a = cmul_rt(a, tw[k * r]);
         } else if constexpr (TWK == 2) {
-          if (r > 0) a = cmulv(a, w[r]);
+          if (r > 0) a = cmul_rt(a, w[r]);
+        } else if constexpr (TWK == 3) {
+          if (r > 0) a = cmul_rt(a, tw[k * R + r]);
         }
         v[rd][r] = a;
       }
       DftV<R>::run(v[rd]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[rd][r] = undef_f2v();
     }
   }
   __syncthreads();
@@ -797,7 +903,7 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
       // first pass: dst = j*16, r < 16; later passes: NS % 16 == 0 -> affine as above
       constexpr bool AFF = (NS == 1) ? (R == 16) : (NS % 16 == 0);
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+      for (int r = 0; r < RS; ++r)
         buf[AFF ? pd + r * (NS + NS / 16) : pidx(dst + r * NS)] = v[rd][r];
     }
   }
@@ -806,13 +912,132 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
 
 // tw: [W_{R0 R1}^e, e < R0 R1] ++ [W_M^k, k < R0 R1]
 // NZ: the input is zero beyond its first NZ elements (per FFT)
-template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M>
+// NO: only outputs k < NO are read afterwards (three-pass plans: the last pass writes k = j + r R0 R1)
+// KR: tw is the [k][r] layout (MfccDev::ftw2) instead of ftw
+template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M, int NO = M, bool KR = false>
 __device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const float2* vhat) {
   static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
+  static_assert(NO == M || R2 > 1, "output pruning needs a third pass");
   constexpr int MR0 = M / R0;
   spass<M, R0, 1, PP, 0, VMUL, (NZ + MR0 - 1) / MR0>(buf, nullptr, vhat);
-  spass<M, R1, R0, PP, 1, false>(buf, tw, nullptr);
-  if constexpr (R2 > 1) spass<M, R2, R0 * R1, PP, 2, false>(buf, tw + R0 * R1, nullptr);
+  spass<M, R1, R0, PP, KR ? 3 : 1, false>(buf, tw, nullptr);
+  if constexpr (R2 > 1)
+    spass<M, R2, R0 * R1, PP, KR ? 3 : 2, false, R2, (NO + R0 * R1 - 1) / (R0 * R1)>(buf, tw + R0 * R1, nullptr);
+}
+
+// Fast-kernel pass with the global loads moved ahead of the barrier: the pass's twiddle / vhat
+// loads are issued BEFORE the barrier that publishes the previous pass's LDS writes (the
+// registers are free there: the previous pass's values are already stored), so their latency
+// overlaps the barrier wait instead of stalling the DFT; then LDS reads -> DFT -> barrier ->
+// writes.  No trailing barrier: the next pass (or the caller) opens with one.
+//   TWK 0: none;  2: W_M^k base (ftw2 pass-3 table column r = 1) + tw_powers;  3: [k][r] table
+//   PF: rows r < PF are prefetched, the rest loaded after the barrier (VGPR budget of 8 blocks/CU)
+constexpr int kPrefetchRows = 8;
+template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R, int RS = R, int PF = kPrefetchRows>
+__device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2* __restrict__ tws,
+                                         const float2* __restrict__ vhats) {
+  static_assert(!(VMUL && TWK != 0), "vhat product and twiddles never share a pass");
+  constexpr int MR = M / R;
+  constexpr int NB = PP * MR;
+  constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
+  f2v* buf = reinterpret_cast<f2v*>(bufs);
+  const f2v* tw = reinterpret_cast<const f2v*>(tws);
+  const f2v* vhat = reinterpret_cast<const f2v*>(vhats);
+  const int tid = ltid();
+  f2v pre[ROUNDS][R];
+#pragma unroll
+  for (int rd = 0; rd < ROUNDS; ++rd) {
+    const int g = min(tid + rd * kThreads, NB - 1);
+    const int f = g / MR;
+    const int j = g - f * MR;
+    const int k = (NS == 1) ? 0 : j % NS;
+    if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (VMUL) pre[rd][r] = (r < ZT && r < PF) ? vhat[j + r * MR] : undef_f2v();
+        else if constexpr (TWK == 3) pre[rd][r] = (r > 0 && r < PF) ? tw[k * R + r] : undef_f2v();
+        else if constexpr (TWK == 2) pre[rd][r] = (r == 1) ? tw[k * R + 1] : undef_f2v();
+        else pre[rd][r] = undef_f2v();
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) pre[rd][r] = undef_f2v();
+    }
+  }
+  __syncthreads();
+  f2v v[ROUNDS][R];
+#pragma unroll
+  for (int rd = 0; rd < ROUNDS; ++rd) {
+    const int g = min(tid + rd * kThreads, NB - 1);
+    if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
+      const int f = g / MR;
+      const int j = g - f * MR;
+      const int rb = f * M + j;
+      const int prb = pidx(rb);
+      const int k = (NS == 1) ? 0 : j % NS;
+      if constexpr (TWK == 2) tw_powers<R>(pre[rd][1], pre[rd]);
+#pragma unroll
+      for (int r = PF; r < R; ++r) {  // rows past the prefetch budget
+        if constexpr (VMUL) {
+          if (r < ZT) pre[rd][r] = vhat[j + r * MR];
+        } else if constexpr (TWK == 3) {
+          pre[rd][r] = tw[k * R + r];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= ZT) {
+          v[rd][r] = f2v{0.0f, 0.0f};
+          continue;
+        }
+        f2v a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
+        if constexpr (VMUL) a = cmul_conj_rt(a, pre[rd][r]);
+        if constexpr (TWK != 0) {
+          if (r > 0) a = cmul_rt(a, pre[rd][r]);
+        }
+        v[rd][r] = a;
+      }
+      DftV<R>::run(v[rd]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[rd][r] = undef_f2v();
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int rd = 0; rd < ROUNDS; ++rd) {
+    const int g = min(tid + rd * kThreads, NB - 1);
+    if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
+      const int f = g / MR;
+      const int j = g - f * MR;
+      const int k = (NS == 1) ? 0 : j % NS;
+      const int dst = f * M + (j - k) * R + k;
+      const int pd = pidx(dst);
+      constexpr bool AFF = (NS == 1) ? (R == 16) : (NS % 16 == 0);
+#pragma unroll
+      for (int r = 0; r < RS; ++r)
+        if (ROUNDS * kThreads == NB || tid + rd * kThreads < NB)
+          buf[AFF ? pd + r * (NS + NS / 16) : pidx(dst + r * NS)] = v[rd][r];
+    }
+  }
+}
+
+// fft_plan over spass_pf with the [k][r] tables (MfccDev::ftw2); no trailing barrier.
+//   ABD_TW3_TABLE: the third pass reads all R2 - 1 factors from the table instead of one base + powers
+#ifdef ABD_TW3_TABLE
+constexpr int kTw3 = 3;
+#else
+constexpr int kTw3 = 2;
+#endif
+template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M, int NO = M>
+__device__ __forceinline__ void fft_plan_pf(float2* buf, const float2* tw, const float2* vhat) {
+  static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
+  static_assert(NO == M || R2 > 1, "output pruning needs a third pass");
+  constexpr int MR0 = M / R0;
+  spass_pf<M, R0, 1, PP, 0, VMUL, (NZ + MR0 - 1) / MR0>(buf, nullptr, vhat);
+  spass_pf<M, R1, R0, PP, 3, false>(buf, tw, nullptr);
+  if constexpr (R2 > 1)
+    spass_pf<M, R2, R0 * R1, PP, kTw3, false, R2, (NO + R0 * R1 - 1) / (R0 * R1)>(buf, tw + R0 * R1, nullptr);
 }
 
 // Injected sample at signal index s (already clamped into [0, L)); branch-free so the
@@ -912,7 +1137,10 @@ __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const floa
       const int idx = ltid() + (g0 + q) * kThreads;
       if ((g0 + q < ITERS) && idx < TOT) {
         float2 z;
-        if constexpr (BLUE) z = cmul(make_float2(a[q], b[q]), c[q]);
+        if constexpr (BLUE) {
+          const f2v zz = cmul_rt(f2v{a[q], b[q]}, f2v{c[q].x, c[q].y});
+          z = make_float2(zz.x, zz.y);
+        }
         else z = make_float2(a[q] * c[q].x, b[q] * c[q].y);
         buf[pidx(idx)] = ok[q] ? z : make_float2(0.0f, 0.0f);
       }
@@ -936,16 +1164,88 @@ __device__ __forceinline__ void load_item(float2* buf, const float* x, const Mfc
 //   -> in-place power |A_k|^2, |B_k|^2 (Bluestein output chirp fused)
 //   -> mel by half-filter slots (2 per filter, balanced), halves combined by a lane swap
 //   -> 10 log10 -> ws_db, per-item max -> ws_max.
-// ABD_TW_LDS: stage the inter-pass twiddle tables (4 KB) in LDS.  Off by default: read through
+// Twiddles are read through the L1 from the [k][r] tables (MfccDev::ftw2): the block's LDS is its
+// FFT buffer alone (19.6 KB for Bluestein), so 8 blocks (32 waves, the CU maximum) fit; the kernel
+// is latency-bound (46 % of wave cycles parked at barriers / waitcnt), so residency is what pays.
 // the L1 instead, the Bluestein block's LDS drops from 23.7 to 19.6 KB and 8 blocks (32 waves, the
 // CU maximum) fit instead of 6 -- the kernel is latency-bound (46 % of wave cycles parked at
 // barriers / waitcnt, profiles/r2_stft_pmc.txt), so the extra residency is what pays.
-#ifdef ABD_TW_LDS
-constexpr bool kTwLds = true;
-#else
-constexpr bool kTwLds = false;
-#endif
-constexpr int kBlueBlocks = kTwLds ? 6 : 8;
+constexpr int kBlueBlocks = 8;
+
+// Bluestein item (one pair of frames) after the second FFT: power -> mel -> dB.
+//   power: bin k of frames a / b from Z[k], Z[N-k] (output chirp fused), written as one float2
+//          per bin into a contiguous array placed past the FFT outputs that are still read
+//          (Z[k], k < N), so the reads and writes need no barrier between them;
+//   mel:   thread = half-filter slot (2 m + h, 2 n_mels == kThreads), kMelHP zero-padded weights
+//          per slot (p.mel3_w), every read base + immediate, one v_pk_fma per bin for both
+//          frames; the halves are combined by a lane swap, lane h writes frame 2 p0 + h.
+constexpr int kMelHP = 16;  // padded bins per half-filter slot of the Bluestein fast path
+template <int M, int NN>
+__device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const MfccDev& p, float* __restrict__ db_u,
+                                                int t0) {
+  constexpr int NF = NN / 2 + 1;
+  constexpr int POFF = ((NN + NN / 16) + 15) / 16 * 16;  // >= pidx(N - 1) + 1
+  static_assert(POFF + NF + kMelHP <= M + M / 16, "power array must fit the FFT buffer");
+  f2v* buf = reinterpret_cast<f2v*>(bufs);
+  f2v* pw = buf + POFF;
+  const f2v* co = reinterpret_cast<const f2v*>(p.chirp_out);
+  constexpr int PR = (NF + kMelHP + kThreads - 1) / kThreads;
+  f2v cq[PR][2];  // output chirps, loaded ahead of the barrier that publishes the last FFT pass
+#pragma unroll
+  for (int rd = 0; rd < PR; ++rd) {
+    const int k = min(ltid() + rd * kThreads, NF - 1);
+    const int kn = (k == 0) ? 0 : NN - k;
+    cq[rd][0] = co[k];
+    cq[rd][1] = co[kn];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int rd = 0; rd < PR; ++rd) {
+    const int k = ltid() + rd * kThreads;
+    if (k < NF + kMelHP) {
+      f2v e = f2v{0.0f, 0.0f};
+      if (k < NF) {
+        const int kn = (k == 0) ? 0 : NN - k;
+        // X[k] = conj(w[k] R[k]) / M  (chirp_out = w / M)
+        f2v P1 = cmul_rt(buf[pidx(k)], cq[rd][0]), Q = cmul_rt(buf[pidx(kn)], cq[rd][1]);
+        P1.y = -P1.y;
+        Q.y = -Q.y;
+        const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
+        const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
+        e = f2v{ar * ar + ai * ai, br * br + bi * bi};
+      }
+      pw[k] = e;  // bins NF .. NF + kMelHP - 1: zeros under the slots' padded weights
+    }
+  }
+  __syncthreads();
+  const int sl = ltid();
+  const int start = p.mel2_meta[sl].x;
+  const float4* wq = reinterpret_cast<const float4*>(p.mel3_w) + sl * (kMelHP / 4);
+  float w[kMelHP];
+#pragma unroll
+  for (int q = 0; q < kMelHP / 4; ++q) {
+    const float4 v = wq[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+  const f2v* ps = pw + start;
+  f2v s = f2v{0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < kMelHP; ++i) s = fmav(ps[i], f2v{w[i], w[i]}, s);
+  s.x += __shfl_xor(s.x, 1);
+  s.y += __shfl_xor(s.y, 1);
+  const int h = sl & 1;
+  const int t = t0 + h;
+  float lmax = -INFINITY;
+  if (t < p.T) {
+    const float d = 10.0f * log10f(fmaxf(h ? s.y : s.x, 1e-10f));
+    db_u[(int64_t)t * p.n_mels + (sl >> 1)] = d;
+    lmax = d;
+  }
+  return lmax;
+}
 
 template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
 __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
@@ -955,11 +1255,10 @@ __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fas
                                                                  float* __restrict__ ws_db,
                                                                  float* __restrict__ ws_max,
                                                                  unsigned* __restrict__ queue) {
-  constexpr int NT = 2 * R0 * R1;
   // first FFT's first pass reads rows r < ceil(N / (M/R0)) only: the rest is never stored
   constexpr int kNZW = (BLUE && PP == 1) ? ((NN + M / R0 - 1) / (M / R0)) * (M / R0) : M;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  constexpr int NTL = kTwLds ? NT : 0;
+  constexpr int NTL = 0;
   float2* buf = lds + NTL;
 #ifdef ABD_MEL_W_LDS
   float* wl = reinterpret_cast<float*>(lds + NTL + PP * (M + M / 16));
@@ -967,9 +1266,7 @@ __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fas
   const float* wl = p.mel2_w;  // 4-5 KB, L1-resident: keeps the block's LDS to its FFT buffer
 #endif
   __shared__ float red[kThreads / kWave];
-  const float2* tw = kTwLds ? lds : p.ftw;
-  if constexpr (kTwLds)
-    for (int i = ltid(); i < NT; i += kThreads) lds[i] = p.ftw[i];
+  const float2* tw = p.ftw2;
 #ifdef ABD_MEL_W_LDS
   for (int i = ltid(); i < p.mel2_total; i += kThreads) wl[i] = p.mel2_w[i];
 #endif
@@ -1027,12 +1324,19 @@ __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fas
         break;
       default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
     }
-    __syncthreads();
+    // no barrier here: the first pass opens with the one that publishes the loaded frames
     if (!(p.ablate & 2)) {
-      fft_plan<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr);
-      if constexpr (BLUE) fft_plan<M, R0, R1, R2, PP, true>(buf, tw, p.vhat);
+      fft_plan_pf<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr);
+      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PP, true, M, NN>(buf, tw, p.vhat);
     }
     float lmax = -INFINITY;
+    if constexpr (BLUE && PP == 1) {
+      if (p.mel3_w != nullptr && !(p.ablate & 4)) {
+        lmax = power_mel_blue<M, NN>(buf, p, ws_db + (int64_t)u * p.T * p.n_mels, 2 * p0);
+        goto item_done;
+      }
+    }
+    __syncthreads();  // the last pass's writes (fft_plan_pf leaves no trailing barrier)
     if (!(p.ablate & 4)) {
       // Power of the two real spectra, written over Z[k] (k <= N/2).  Z[k] is read only by
       // the thread that owns bin k (Z[N-k] with N-k > N/2 is never written), so no barrier
@@ -1088,6 +1392,7 @@ __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fas
         }
       }
     }
+  item_done:
     lmax = abd::wave_max(lmax);
     if ((ltid() & 63) == 0) red[ltid() / kWave] = lmax;
     __syncthreads();
@@ -1382,7 +1687,7 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
                 hipStream_t s) {
   auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE>;
   static_assert(M % 16 == 0, "padded LDS layout needs M % 16 == 0");
-  size_t lds = (size_t)((kTwLds ? 2 * R0 * R1 : 0) + PP * (M + M / 16)) * sizeof(float2);
+  size_t lds = (size_t)(PP * (M + M / 16)) * sizeof(float2);
 #ifdef ABD_MEL_W_LDS
   lds += (size_t)((d.mel2_total + 3) & ~3) * 4;
 #endif
@@ -1704,6 +2009,12 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   }
   d.mel2_total = (int)mw2.size();
   d.mel2_hp = std::max(8, (hmax + 7) / 8 * 8);
+  // padded slot weights for the Bluestein fast path (power_mel_blue): one slot per thread
+  const bool mel3 = blue && d.fast && 2 * n_mels == kThreads && hmax <= kMelHP;
+  std::vector<float> mw3(mel3 ? (size_t)2 * n_mels * kMelHP : 0, 0.0f);
+  if (mel3)
+    for (int sl = 0; sl < 2 * n_mels; ++sl)
+      for (int i = 0; i < meta2[sl].y; ++i) mw3[(size_t)sl * kMelHP + i] = mw2[meta2[sl].z + i];
   // fast-kernel twiddles: W_{R0 R1}^e and W_M^k, e, k < R0 R1
   const int r01 = fp ? fp->r0 * fp->r1 : 1;
   std::vector<float2> ftw(2 * (size_t)r01);
@@ -1712,6 +2023,21 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     ftw[e] = make_float2((float)cos(a), (float)sin(a));
     ftw[r01 + e] = make_float2((float)cos(b), (float)sin(b));
   }
+  std::vector<float2> ftw2;
+  if (fp) {
+    const int r0 = fp->r0, r1 = fp->r1, r2 = M / (r0 * r1);
+    for (int k = 0; k < r0; ++k)
+      for (int r = 0; r < r1; ++r) {
+        const double a = -2.0 * M_PI * (double)((k * r) % r01) / r01;
+        ftw2.push_back(make_float2((float)cos(a), (float)sin(a)));
+      }
+    for (int k = 0; k < r01; ++k)
+      for (int r = 0; r < r2; ++r) {
+        const double a = -2.0 * M_PI * (double)(((int64_t)k * r) % M) / M;
+        ftw2.push_back(make_float2((float)cos(a), (float)sin(a)));
+      }
+  }
+  if (ftw2.empty()) ftw2.push_back(make_float2(1.0f, 0.0f));
   std::vector<float> dct((size_t)n_mels * n_mfcc);
   for (int m = 0; m < n_mels; ++m)
     for (int c = 0; c < n_mfcc; ++c) {
@@ -1719,6 +2045,20 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
       if (c == 0) v *= 1.0 / sqrt(2.0);
       dct[(size_t)m * n_mfcc + c] = (float)v;
     }
+  // B fragments of db_dct_mfma_kernel: [s][q][tile][col] -> float4 over j of dct[16 s + 4 q + j][16 tile + col]
+  d.dct_tiles = (n_mels % 16 == 0 && n_mfcc <= 48 && getenv("ABD_DCT_NOMFMA") == nullptr) ? (n_mfcc + 15) / 16 : 0;
+  std::vector<float4> dfrag;
+  if (d.dct_tiles > 0)
+    for (int sg = 0; sg < n_mels / 16; ++sg)
+      for (int q = 0; q < 4; ++q)
+        for (int tile = 0; tile < d.dct_tiles; ++tile)
+          for (int col = 0; col < 16; ++col) {
+            const int c = 16 * tile + col;
+            float e[4];
+            for (int j = 0; j < 4; ++j) e[j] = c < n_mfcc ? dct[(size_t)(16 * sg + 4 * q + j) * n_mfcc + c] : 0.0f;
+            dfrag.push_back(make_float4(e[0], e[1], e[2], e[3]));
+          }
+  if (dfrag.empty()) dfrag.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
 
   // ---- one device block for every table
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1743,10 +2083,16 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   sz += al(dct.size() * sizeof(float));
   size_t off_ftw = sz;
   sz += al(ftw.size() * sizeof(float2));
+  size_t off_dfrag = sz;
+  sz += al(dfrag.size() * sizeof(float4));
+  size_t off_ftw2 = sz;
+  sz += al(ftw2.size() * sizeof(float2));
   size_t off_m2 = sz;
   sz += al(meta2.size() * sizeof(int4));
   size_t off_w2 = sz;
   sz += al(mw2.size() * sizeof(float));
+  size_t off_w3 = sz;
+  sz += al(mw3.size() * sizeof(float));
   size_t off_bm = sz;
   sz += al(nf * sizeof(int2));
   size_t off_bw = sz;
@@ -1765,8 +2111,11 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   memcpy(&host[off_mw], mw.data(), mw.size() * sizeof(float));
   memcpy(&host[off_dct], dct.data(), dct.size() * sizeof(float));
   memcpy(&host[off_ftw], ftw.data(), ftw.size() * sizeof(float2));
+  memcpy(&host[off_dfrag], dfrag.data(), dfrag.size() * sizeof(float4));
+  memcpy(&host[off_ftw2], ftw2.data(), ftw2.size() * sizeof(float2));
   memcpy(&host[off_m2], meta2.data(), meta2.size() * sizeof(int4));
   memcpy(&host[off_w2], mw2.data(), mw2.size() * sizeof(float));
+  if (!mw3.empty()) memcpy(&host[off_w3], mw3.data(), mw3.size() * sizeof(float));
   hipError_t e = hipMalloc(&pl->block, sz);
   if (e != hipSuccess) {
     delete pl;
@@ -1792,8 +2141,11 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.mel_w = reinterpret_cast<const float*>(b + off_mw);
   d.dct = reinterpret_cast<const float*>(b + off_dct);
   d.ftw = reinterpret_cast<const float2*>(b + off_ftw);
+  d.dct_frag = reinterpret_cast<const float4*>(b + off_dfrag);
+  d.ftw2 = reinterpret_cast<const float2*>(b + off_ftw2);
   d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
   d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
+  d.mel3_w = mw3.empty() || getenv("ABD_MEL_GENERIC") ? nullptr : reinterpret_cast<const float*>(b + off_w3);
   d.bin_mel = reinterpret_cast<const int2*>(b + off_bm);
   d.bin_w = reinterpret_cast<const float2*>(b + off_bw);
   *plan = pl;
@@ -1902,7 +2254,12 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   ABD_LAUNCH_CHECK();
   abd::prof_begin(abd::PH_DB_DCT, s);
   const size_t dct_lds = ((size_t)d.n_mels * d.n_mfcc + (size_t)kTT2 * d.n_mels) * sizeof(float);
-  if (d.n_mfcc % 4 == 0 && dct_lds <= 64 * 1024 &&
+  if (d.dct_tiles > 0) {
+    const dim3 g((unsigned)batch, (unsigned)((d.T + 63) / 64));
+    if (d.dct_tiles == 1) db_dct_mfma_kernel<1><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
+    else if (d.dct_tiles == 2) db_dct_mfma_kernel<2><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
+    else db_dct_mfma_kernel<3><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
+  } else if (d.n_mfcc % 4 == 0 && dct_lds <= 64 * 1024 &&
       (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
       getenv("ABD_DCT_GENERIC") == nullptr) {
     db_dct_lds_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT2 - 1) / kTT2)), dim3(kThreads), dct_lds, s>>>(
