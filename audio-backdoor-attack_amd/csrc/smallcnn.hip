@@ -1271,7 +1271,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // accuracy at 6 x 32 MFMA cycles per 16-deep k-step instead of 8 x 64 for v_mfma_f32_32x32x2_f32.
 // MI = 32-row m-tiles per wave (block rows 128 * MI): MI = 2 halves the LDS reads per MFMA
 // (2 A + 2 B fragments per plane feed 4 accumulators), which the 3-plane split is bound by.
-template <int NB, int EPI, int KB, int NP = 1, int MI = 1>
+// PD = 2: operand loads run two K chunks ahead (two register sets): the first tap of a chunk
+// streams x1 from HBM (~2 us latency), which one chunk of MFMAs (24 x 32 cycles) cannot cover.
+template <int NB, int EPI, int KB, int NP = 1, int MI = 1, int PD = 1>
 __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   static_assert(NP == 1 || NP == 3, "1 (bf16) or 3 (exact fp32 split) planes");
   constexpr int BM = kBM * MI, LD = KB + 8, Q = KB / 4;  // Q float4 per row
@@ -1321,8 +1323,8 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
   }
   const int cpt = a.Cs / KB;
   const int nch = a.taps * cpt;
-  float4 ra[RPT], rbv[BPT];
-  auto load = [&](int ch) {
+  float4 ras[PD][RPT], rbs[PD][BPT];
+  auto load = [&](int ch, float4* ra, float4* rbv) {
     const int t = ch / cpt;
     const int c0 = (ch - t * cpt) * KB;
     const uint32_t adelta = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * a.Cs + c0) * 4);
@@ -1362,14 +1364,16 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  load(0);
-  for (int ch = 0; ch < nch; ++ch) {
+  // one K chunk: stage register set `slot` into LDS, refill it PD chunks ahead, MFMAs
+  auto chunk = [&](int ch, int slot) {
+    float4* ra = ras[slot];
+    float4* rbv = rbs[slot];
 #pragma unroll
     for (int i = 0; i < RPT; ++i) put(&As[0][(r0 + RSTEP * i) * LD + 4 * q], BM * LD, ra[i]);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) put(&Bs[0][(r0 + RSTEP * j) * LD + 4 * q], NB * LD, rbv[j]);
     __syncthreads();
-    if (ch + 1 < nch) load(ch + 1);
+    if (ch + PD < nch) load(ch + PD, ra, rbv);
     const int aoff = (wave * 32 * MI + (lane & 31)) * LD + 8 * (lane >> 5);
     const int boff = (lane & 31) * LD + 8 * (lane >> 5);
 #pragma unroll
@@ -1398,6 +1402,14 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
       }
     }
     __syncthreads();
+  };
+#pragma unroll
+  for (int sl = 0; sl < PD; ++sl)
+    if (sl < nch) load(sl, ras[sl], rbs[sl]);
+  for (int ch = 0; ch < nch; ch += PD) {
+#pragma unroll
+    for (int sl = 0; sl < PD; ++sl)
+      if (ch + sl < nch) chunk(ch + sl, sl);
   }
   // epilogue (same maps as the fp32 kernel): row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31
   float st[NJ][2];
@@ -1444,6 +1456,211 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
       }
       a.part[((int64_t)0 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s0;
       a.part[((int64_t)1 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s1;
+    }
+  }
+}
+
+// Weight-stationary 2x2 conv GEMM, 3-plane split (ABD_PREC_F32_SPLIT), Cs = N = 64, 4 taps, K = 256:
+// conv2 forward (EPI_CONV: bias + ReLU + BN2 statistics) and data gradient (EPI_STORE).
+//   * the whole weight operand (64 x 256, three exact bf16 planes, 101 KB with conflict-free
+//     528-B rows) is staged into LDS ONCE per block: one persistent 512-thread block per CU;
+//   * every wave owns a contiguous 1/(8 grid) share of the output rows and walks it in 64-row x
+//     64-column tiles (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators) with no block barrier:
+//     its A fragments (8 consecutive channels of one tap-shifted source row per lane) come
+//     straight from global memory through buffer loads (an out-of-grid tap reads zeros via the
+//     descriptor's range check), are split into three bf16 planes in registers and fed to the
+//     MFMAs; the K loop (4 taps x 4 channel groups of 16) is unrolled with loads two steps ahead.
+// Same six-term product as gemm_nt_bf16_kernel<.., NP = 3> (a2b0 + a0b2 + a1b1 + a1b0 + a0b1 +
+// a0b0 per 16-deep step), so the GEMM keeps fp32 accuracy; only the summation grouping differs.
+constexpr int kWsWaves = 8, kWsT = kWsWaves * 64;
+constexpr int kWsLD = 256 + 8;  // bf16 per staged weight row (528 B: 16 lanes of a ds_read_b128 hit distinct banks)
+__device__ __forceinline__ void split3_x8(const float4& lo, const float4& hi, bf16x8* pl) {
+  const f32x2 in[4] = {f32x2{lo.x, lo.y}, f32x2{lo.z, lo.w}, f32x2{hi.x, hi.y}, f32x2{hi.z, hi.w}};
+  uint32_t u[3][4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    f32x2 x = in[h];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const bf16x2 r = __builtin_convertvector(x, bf16x2);
+      u[q][h] = __builtin_bit_cast(uint32_t, r);
+      if (q < 2) {
+        const f32x2 back = {__builtin_bit_cast(float, u[q][h] << 16), __builtin_bit_cast(float, u[q][h] & 0xffff0000u)};
+        x -= back;  // exact: x - rne(x) fits in fp32
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) pl[q] = __builtin_bit_cast(bf16x8, make_uint4(u[q][0], u[q][1], u[q][2], u[q][3]));
+}
+
+template <int EPI, int PDW = 4>  // PDW: K steps the A loads run ahead (register ring of PDW slots)
+__global__ void __launch_bounds__(kWsT, 1) conv_ws_split_kernel(NTArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][64 * kWsLD];
+  __shared__ float red[kWsWaves][64][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // ---- weights -> three exact bf16 planes, [plane][n][k] with k = tap * 64 + channel
+  for (int idx = tid; idx < 64 * 32; idx += kWsT) {
+    const int n = idx >> 5, k8 = (idx & 31) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    bf16x8 pl[3];
+    split3_x8(lo, hi, pl);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * kWsLD + k8]) = pl[q];
+  }
+  __syncthreads();
+  // ---- this wave's rows [r_lo, r_hi): an even split of M over every wave of the grid
+  const int64_t W = (int64_t)gridDim.x * kWsWaves;
+  const int64_t g = (int64_t)blockIdx.x * kWsWaves + __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (SGPR)
+  const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
+  const int HoWo = a.Ho * a.Wo;
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)a.Hs * a.Ws * 64 * 4 * (a.M / HoWo), 0x7ffffff0),
+      0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const int kq = 8 * (lane >> 5);  // this lane's 8 channels / k inside a 16-deep step
+  float st[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  float bias[2] = {0.f, 0.f};
+  if constexpr (EPI == EPI_CONV) {
+    bias[0] = a.bias[lane & 31];
+    bias[1] = a.bias[32 + (lane & 31)];
+  }
+  // One continuous stream of K steps over all of this wave's tiles (16 steps per 64-row tile):
+  // the A loads run PDW steps ahead ACROSS tile boundaries, so the pipeline never drains at a
+  // tile's epilogue.  li: byte offsets (tap 0, channel kq) + tap-validity masks of the two A rows
+  // of the tile the loads are in.
+  struct RowInfo {
+    uint32_t roff[2], tm[2];
+  };
+  auto rows_of = [&](int m0) {
+    RowInfo r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + 32 * i + (lane & 31);
+      const bool ok = m < r_hi;
+      const int mm = ok ? m : r_lo;
+      const int b = mm / HoWo, rem = mm - b * HoWo;
+      const int h = rem / a.Wo, w = rem - h * a.Wo;
+      r.roff[i] = (uint32_t)((((int64_t)b * a.Hs + h) * a.Ws + w) * 64 + kq) * 4u;
+      uint32_t mk = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int hs = h + a.dh[t], ws = w + a.dw[t];
+        if (ok && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
+      }
+      r.tm[i] = mk;
+    }
+    return r;
+  };
+  const int ntiles = (r_hi - r_lo + 63) / 64;
+  // this wave's output rows [r_lo, r_hi) as one buffer (ldc == 64 checked by the launcher)
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.out + (int64_t)r_lo * 64, 0, (r_hi - r_lo) * 64 * 4, 0x00020000);
+  if (ntiles > 0) {
+    float4 raw[PDW][2][2];  // [slot][i][lo/hi]: slot ks % PDW, refilled with the step PDW later once split
+    auto load = [&](const RowInfo& li, int ks, float4 (&r)[2][2]) {
+      const int t = ks >> 2, c16 = ks & 3;
+      const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * 64 + c16 * 16) * 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t off = ((li.tm[i] >> t) & 1u) ? li.roff[i] + tofs : kOOB;
+        r[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
+        r[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
+      }
+    };
+    f32x16 acc[2][2];
+    auto step = [&](int ks, float4 (&r)[2][2], const RowInfo& li, int lks) {
+      bf16x8 av[2][3], bv[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) split3_x8(r[i][0], r[i][1], av[i]);
+      // keep the refill behind the split: hoisted above it, the loads need fresh registers and
+      // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
+      __builtin_amdgcn_sched_barrier(0);
+      load(li, lks, r);  // unconditional: a conditional refill is a phi (copies)
+      const int kb = (ks >> 2) * 64 + (ks & 3) * 16 + kq;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * kWsLD + kb]);
+      // term-major: four independent accumulator chains between dependent MFMAs
+      constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
+#pragma unroll
+      for (int term = 0; term < 6; ++term)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
+    };
+    RowInfo li = rows_of(r_lo);
+#pragma unroll
+    for (int sl = 0; sl < PDW; ++sl) load(li, sl, raw[sl]);
+#pragma unroll 1
+    for (int tile = 0; tile < ntiles; ++tile) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+      // one tile = 16 unrolled K steps; the last PDW steps load the next tile's first PDW steps
+      // (past the last tile they re-read this tile's final step: harmless, never consumed)
+      const bool more = tile + 1 < ntiles;
+      const RowInfo cur = li;
+      li = rows_of(r_lo + 64 * (more ? tile + 1 : tile));  // unconditional (no branch in the stream)
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        if (ks + PDW < 16) step(ks, raw[ks % PDW], cur, ks + PDW);
+        else step(ks, raw[ks % PDW], li, more ? ks + PDW - 16 : 15);
+      }
+      {
+        // branch-free: rows past r_hi store to an out-of-range buffer offset (dropped by the range
+        // check), so the waitcnt pass can count the stores and keep the next tile's loads in flight
+        const int m0 = r_lo + 64 * tile;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const bool ok = m < r_hi;
+            const uint32_t ob = ok ? (uint32_t)((m - r_lo) * 64 + (lane & 31)) * 4u : kOOB;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              float v = acc[i][j][r];
+              if constexpr (EPI == EPI_CONV) {
+                v = fmaxf(v + bias[j], 0.0f);
+                const float vs = ok ? v : 0.0f;
+                st[j][0] += vs;
+                st[j][1] = fmaf(vs, vs, st[j][1]);
+              }
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
+            }
+          }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_CONV) {
+    if (a.part == nullptr) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+      const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+      if (lane < 32) {
+        red[wave][32 * j + lane][0] = s0;
+        red[wave][32 * j + lane][1] = s1;
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float s0 = 0.0f, s1 = 0.0f;
+      for (int w = 0; w < kWsWaves; ++w) {
+        s0 += red[w][tid][0];
+        s1 += red[w][tid][1];
+      }
+      a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
+      a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
     }
   }
 }
@@ -2469,6 +2686,35 @@ int launch_conv_halo_split(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
+// conv_ws_split_kernel: one persistent block per CU (ABD_WS=0 restores gemm_nt_bf16_kernel)
+int ws_grid() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    n = std::max(1, cu);
+  }
+  return n;
+}
+bool ws_on() {
+  static const bool on = env_int("ABD_WS", 1) != 0;
+  return on;
+}
+template <int EPI>
+int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
+  if (!ws_on() || a.Cs != 64 || a.N != 64 || a.taps != 4 || a.ksplit > 1 || a.ldb != 256 || a.ldc != 64) return -1;
+  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != ws_grid()) return -1;
+  if ((int64_t)a.Hs * a.Ws * 64 * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
+  if (phase >= 0) abd::prof_begin(phase, s);
+  static const int pdw = env_int("ABD_WS_PD", 4);
+  if (pdw == 2) conv_ws_split_kernel<EPI, 2><<<dim3(ws_grid()), dim3(kWsT), 0, s>>>(a);
+  else conv_ws_split_kernel<EPI, 4><<<dim3(ws_grid()), dim3(kWsT), 0, s>>>(a);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
 // K-chunk depth of the 3-plane conv2 GEMMs (ABD_SPLIT_KB=16: 28 KB of LDS per block, 4 waves/SIMD)
 static int split_kb() {
   static const int kb = env_int("ABD_SPLIT_KB", 32) == 16 ? 16 : 32;
@@ -2481,13 +2727,20 @@ static int split_mi() {
   return mi;
 }
 
+// prefetch distance of the 3-plane GEMMs (ABD_SPLIT_PD=1: loads one chunk ahead)
+static int split_pd() {
+  static const int pd = env_int("ABD_SPLIT_PD", 2) == 1 ? 1 : 2;
+  return pd;
+}
+
 template <int NB, int EPI, int KB, int NP = 1, int MI = 1>
 int launch_nt_bf16(const NTArgs& a, hipStream_t s, int phase) {
   if (a.Cs % KB != 0 || a.ksplit > 1) return -1;
   if (EPI == EPI_CONV && a.part != nullptr && a.nblk != (a.M + kBM * MI - 1) / (kBM * MI)) return -1;
   dim3 grid((a.M + kBM * MI - 1) / (kBM * MI), (a.N + NB - 1) / NB, 1);
   if (phase >= 0) abd::prof_begin(phase, s);
-  gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI><<<grid, dim3(kT), 0, s>>>(a);
+  if (NP == 3 && split_pd() == 2) gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI, 2><<<grid, dim3(kT), 0, s>>>(a);
+  else gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI, 1><<<grid, dim3(kT), 0, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -2662,12 +2915,15 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
+    const bool ws = sp && ws_on();
     a.nblk = bf ? (a.M + kBM - 1) / kBM
+             : ws ? ws_grid()
              : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
              : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
+           : ws ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD)
            : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
                    : launch_conv_halo_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD) == 0
                        ? 0
@@ -2914,6 +3170,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
         : net->precision == ABD_PREC_F32_SPLIT
             ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
+               : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0 ? 0
                : launch_conv_halo_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0
                    ? 0
                : split_kb() == 16 ? launch_nt_bf16<64, EPI_STORE, 16, 3>(da, s, abd::PH_CONV2_DGRAD)

@@ -1,13 +1,14 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + PMC passes over a short bench run (one counter group per pass).
-set -e
+# PMC passes over a short bench run (one pass per run): bash scripts/pmc_bench.sh TAG [extra env]
+set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/pmcb
+O=$R/gpurun_out/pmcb_${1:-x}
 mkdir -p $O
-CMD="python3 $R/bench.py --steps 3 --warmup 2 --profile-steps 1 --no-cpu"
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/kt -o kt -f csv -- $CMD > $O/kt.log 2>&1
-timeout -k 10 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d $O/p1 -o p1 -f csv -- $CMD > $O/p1.log 2>&1
-timeout -k 10 180 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA -d $O/p2 -o p2 -f csv -- $CMD > $O/p2.log 2>&1
-timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE -d $O/p3 -o p3 -f csv -- $CMD > $O/p3.log 2>&1
-timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE -d $O/p4 -o p4 -f csv -- $CMD > $O/p4.log 2>&1
+B="python3 $R/bench.py --steps 3 --warmup 2 --profile-steps 1 --no-cpu"
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d $O/b1 -o b1 -f csv -- $B > $O/b1.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $O/b2 -o b2 -f csv -- $B > $O/b2.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d $O/b5 -o b5 -f csv -- $B > $O/b5.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/b3 -o b3 -f csv -- $B > $O/b3.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/b4 -o b4 -f csv -- $B > $O/b4.log 2>&1
+echo "pmc rc $?"

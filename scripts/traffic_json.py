@@ -17,9 +17,9 @@ import sys
 
 PHASE_KERNELS = {
     "stft_mel": "stft_mel_fast_kernel<2304, 1103",
-    "db_dct": "db_dct_lds_kernel",
-    "conv2_fwd": ("gemm_nt_kernel<64, 1, 1>", "gemm_nt_bf16_kernel<64, 1, 32, 3, 1>"),
-    "conv2_dgrad": ("gemm_nt_kernel<64, 0, 1>", "gemm_nt_bf16_kernel<64, 0, 32, 3, 1>"),
+    "db_dct": ("db_dct_lds_kernel", "db_dct_mfma_kernel"),
+    "conv2_fwd": ("gemm_nt_kernel<64, 1, 1>", "gemm_nt_bf16_kernel<64, 1, 32, 3, 1>", "conv_ws_split_kernel<1"),
+    "conv2_dgrad": ("gemm_nt_kernel<64, 0, 1>", "gemm_nt_bf16_kernel<64, 0, 32, 3, 1>", "conv_ws_split_kernel<0"),
     "conv2_wgrad": "conv_wgrad_rows_kernel<64, 64>",
     "conv1_bwd_wgrad": "conv1_wgrad_kernel",
     "bn2_bwd": "bn_bwd_apply_kernel",
