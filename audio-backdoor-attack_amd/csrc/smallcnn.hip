@@ -1472,8 +1472,8 @@ __global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
 //     MFMAs; the K loop (4 taps x 4 channel groups of 16) is unrolled with loads two steps ahead.
 // Same six-term product as gemm_nt_bf16_kernel<.., NP = 3> (a2b0 + a0b2 + a1b1 + a1b0 + a0b1 +
 // a0b0 per 16-deep step), so the GEMM keeps fp32 accuracy; only the summation grouping differs.
-constexpr int kWsWaves = 8, kWsT = kWsWaves * 64;
-constexpr int kWsLD = 256 + 8;  // bf16 per staged weight row (528 B: 16 lanes of a ds_read_b128 hit distinct banks)
+// LDS weight rows are K + 8 bf16 (528 B at K = 256, 272 B at K = 128): the 16 lanes of a
+// ds_read_b128 phase start 4 banks apart, conflict-free.
 __device__ __forceinline__ void split3_x8(const float4& lo, const float4& hi, bf16x8* pl) {
   const f32x2 in[4] = {f32x2{lo.x, lo.y}, f32x2{lo.z, lo.w}, f32x2{hi.x, hi.y}, f32x2{hi.z, hi.w}};
   uint32_t u[3][4];
@@ -1494,55 +1494,64 @@ __device__ __forceinline__ void split3_x8(const float4& lo, const float4& hi, bf
   for (int q = 0; q < 3; ++q) pl[q] = __builtin_bit_cast(bf16x8, make_uint4(u[q][0], u[q][1], u[q][2], u[q][3]));
 }
 
-template <int EPI, int PDW = 4>  // PDW: K steps the A loads run ahead (register ring of PDW slots)
-__global__ void __launch_bounds__(kWsT, 1) conv_ws_split_kernel(NTArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][64 * kWsLD];
-  __shared__ float red[kWsWaves][64][2];
+// Template parameters: NJ = N / 32 output-channel tiles, CS = input channels (K = 4 CS), MI = 32-row
+// A fragments per wave tile, PDW = K steps the A loads run ahead (register ring of PDW slots),
+// WPB = waves per block.  conv2: <2, 64, 2> (101 KB of weights, one 8-wave block per CU);
+// conv3 forward <1, 64, 1> and data gradient <2, 32, 1> (48 KB, smaller tiles for their
+// 150-180 k rows).
+template <int EPI, int NJ, int CS, int MI, int PDW, int WPB>
+__global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
+  constexpr int N = 32 * NJ, K = 4 * CS, LD = K + 8, KS = K / 16, TR = 32 * MI;
+  static_assert(KS % PDW == 0, "a tile's K steps must be a whole number of ring turns");
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][N * LD];
+  __shared__ float red[WPB][N][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // ---- weights -> three exact bf16 planes, [plane][n][k] with k = tap * 64 + channel
-  for (int idx = tid; idx < 64 * 32; idx += kWsT) {
-    const int n = idx >> 5, k8 = (idx & 31) * 8;
+  // ---- weights -> three exact bf16 planes, [plane][n][k] with k = tap * CS + channel
+  for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
+    const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
     const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
     const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
     bf16x8 pl[3];
     split3_x8(lo, hi, pl);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * kWsLD + k8]) = pl[q];
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
   }
   __syncthreads();
   // ---- this wave's rows [r_lo, r_hi): an even split of M over every wave of the grid
-  const int64_t W = (int64_t)gridDim.x * kWsWaves;
-  const int64_t g = (int64_t)blockIdx.x * kWsWaves + __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (SGPR)
+  const int64_t W = (int64_t)gridDim.x * WPB;
+  const int64_t g = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (SGPR)
   const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
   const int HoWo = a.Ho * a.Wo;
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)a.Hs * a.Ws * 64 * 4 * (a.M / HoWo), 0x7ffffff0),
+      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)a.Hs * a.Ws * CS * 4 * (a.M / HoWo), 0x7ffffff0),
       0x00020000);
   constexpr uint32_t kOOB = 0x80000000u;
   const int kq = 8 * (lane >> 5);  // this lane's 8 channels / k inside a 16-deep step
-  float st[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  float bias[2] = {0.f, 0.f};
-  if constexpr (EPI == EPI_CONV) {
-    bias[0] = a.bias[lane & 31];
-    bias[1] = a.bias[32 + (lane & 31)];
+  float st[NJ][2];
+  float bias[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    st[j][0] = st[j][1] = 0.0f;
+    bias[j] = 0.0f;
+    if constexpr (EPI == EPI_CONV) bias[j] = a.bias[32 * j + (lane & 31)];
   }
-  // One continuous stream of K steps over all of this wave's tiles (16 steps per 64-row tile):
+  // One continuous stream of K steps over all of this wave's tiles (KS steps per TR-row tile):
   // the A loads run PDW steps ahead ACROSS tile boundaries, so the pipeline never drains at a
-  // tile's epilogue.  li: byte offsets (tap 0, channel kq) + tap-validity masks of the two A rows
+  // tile's epilogue.  li: byte offsets (tap 0, channel kq) + tap-validity masks of the MI A rows
   // of the tile the loads are in.
   struct RowInfo {
-    uint32_t roff[2], tm[2];
+    uint32_t roff[MI], tm[MI];
   };
   auto rows_of = [&](int m0) {
     RowInfo r;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const int m = m0 + 32 * i + (lane & 31);
       const bool ok = m < r_hi;
       const int mm = ok ? m : r_lo;
       const int b = mm / HoWo, rem = mm - b * HoWo;
       const int h = rem / a.Wo, w = rem - h * a.Wo;
-      r.roff[i] = (uint32_t)((((int64_t)b * a.Hs + h) * a.Ws + w) * 64 + kq) * 4u;
+      r.roff[i] = (uint32_t)((((int64_t)b * a.Hs + h) * a.Ws + w) * CS + kq) * 4u;
       uint32_t mk = 0;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1553,45 +1562,45 @@ __global__ void __launch_bounds__(kWsT, 1) conv_ws_split_kernel(NTArgs a) {
     }
     return r;
   };
-  const int ntiles = (r_hi - r_lo + 63) / 64;
-  // this wave's output rows [r_lo, r_hi) as one buffer (ldc == 64 checked by the launcher)
+  const int ntiles = (r_hi - r_lo + TR - 1) / TR;
+  // this wave's output rows [r_lo, r_hi) as one buffer (ldc == N checked by the launcher)
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-      a.out + (int64_t)r_lo * 64, 0, (r_hi - r_lo) * 64 * 4, 0x00020000);
+      a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
   if (ntiles > 0) {
-    float4 raw[PDW][2][2];  // [slot][i][lo/hi]: slot ks % PDW, refilled with the step PDW later once split
-    auto load = [&](const RowInfo& li, int ks, float4 (&r)[2][2]) {
-      const int t = ks >> 2, c16 = ks & 3;
-      const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * 64 + c16 * 16) * 4);
+    float4 raw[PDW][MI][2];  // [slot][i][lo/hi]: slot ks % PDW, refilled with the step PDW later once split
+    auto load = [&](const RowInfo& li, int ks, float4 (&r)[MI][2]) {
+      const int t = ks / (CS / 16), c16 = ks % (CS / 16);
+      const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * CS + c16 * 16) * 4);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < MI; ++i) {
         const uint32_t off = ((li.tm[i] >> t) & 1u) ? li.roff[i] + tofs : kOOB;
         r[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
         r[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
       }
     };
-    f32x16 acc[2][2];
-    auto step = [&](int ks, float4 (&r)[2][2], const RowInfo& li, int lks) {
-      bf16x8 av[2][3], bv[2][3];
+    f32x16 acc[MI][NJ];
+    auto step = [&](int ks, float4 (&r)[MI][2], const RowInfo& li, int lks) {
+      bf16x8 av[MI][3], bv[NJ][3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) split3_x8(r[i][0], r[i][1], av[i]);
+      for (int i = 0; i < MI; ++i) split3_x8(r[i][0], r[i][1], av[i]);
       // keep the refill behind the split: hoisted above it, the loads need fresh registers and
       // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
       __builtin_amdgcn_sched_barrier(0);
       load(li, lks, r);  // unconditional: a conditional refill is a phi (copies)
-      const int kb = (ks >> 2) * 64 + (ks & 3) * 16 + kq;
+      const int kb = ks * 16 + kq;  // k = tap * CS + channel, 16 per step
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * kWsLD + kb]);
-      // term-major: four independent accumulator chains between dependent MFMAs
+          bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
+      // term-major: independent accumulator chains between dependent MFMAs
       constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
 #pragma unroll
       for (int term = 0; term < 6; ++term)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
     };
     RowInfo li = rows_of(r_lo);
@@ -1600,51 +1609,49 @@ __global__ void __launch_bounds__(kWsT, 1) conv_ws_split_kernel(NTArgs a) {
 #pragma unroll 1
     for (int tile = 0; tile < ntiles; ++tile) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-      // one tile = 16 unrolled K steps; the last PDW steps load the next tile's first PDW steps
-      // (past the last tile they re-read this tile's final step: harmless, never consumed)
+      // KS unrolled K steps; the last PDW load the next tile's first PDW steps (past the last
+      // tile they re-read this tile's final step: harmless, never consumed)
       const bool more = tile + 1 < ntiles;
       const RowInfo cur = li;
-      li = rows_of(r_lo + 64 * (more ? tile + 1 : tile));  // unconditional (no branch in the stream)
+      li = rows_of(r_lo + TR * (more ? tile + 1 : tile));  // unconditional (no branch in the stream)
 #pragma unroll
-      for (int ks = 0; ks < 16; ++ks) {
-        if (ks + PDW < 16) step(ks, raw[ks % PDW], cur, ks + PDW);
-        else step(ks, raw[ks % PDW], li, more ? ks + PDW - 16 : 15);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + PDW < KS) step(ks, raw[ks % PDW], cur, ks + PDW);
+        else step(ks, raw[ks % PDW], li, more ? ks + PDW - KS : KS - 1);
       }
-      {
-        // branch-free: rows past r_hi store to an out-of-range buffer offset (dropped by the range
-        // check), so the waitcnt pass can count the stores and keep the next tile's loads in flight
-        const int m0 = r_lo + 64 * tile;
+      // branch-free epilogue: rows past r_hi store to an out-of-range buffer offset (dropped by
+      // the range check), so the waitcnt pass can count the stores and keep the loads in flight
+      const int m0 = r_lo + TR * tile;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const bool ok = m < r_hi;
-            const uint32_t ob = ok ? (uint32_t)((m - r_lo) * 64 + (lane & 31)) * 4u : kOOB;
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const bool ok = m < r_hi;
+          const uint32_t ob = ok ? (uint32_t)((m - r_lo) * N + (lane & 31)) * 4u : kOOB;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              float v = acc[i][j][r];
-              if constexpr (EPI == EPI_CONV) {
-                v = fmaxf(v + bias[j], 0.0f);
-                const float vs = ok ? v : 0.0f;
-                st[j][0] += vs;
-                st[j][1] = fmaf(vs, vs, st[j][1]);
-              }
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
+          for (int j = 0; j < NJ; ++j) {
+            float v = acc[i][j][r];
+            if constexpr (EPI == EPI_CONV) {
+              v = fmaxf(v + bias[j], 0.0f);
+              const float vs = ok ? v : 0.0f;
+              st[j][0] += vs;
+              st[j][1] = fmaf(vs, vs, st[j][1]);
             }
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
           }
-      }
+        }
     }
   }
   if constexpr (EPI == EPI_CONV) {
     if (a.part == nullptr) return;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
       const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
       if (lane < 32) {
@@ -1653,9 +1660,9 @@ __global__ void __launch_bounds__(kWsT, 1) conv_ws_split_kernel(NTArgs a) {
       }
     }
     __syncthreads();
-    if (tid < 64) {
+    if (tid < N) {
       float s0 = 0.0f, s1 = 0.0f;
-      for (int w = 0; w < kWsWaves; ++w) {
+      for (int w = 0; w < WPB; ++w) {
         s0 += red[w][tid][0];
         s1 += red[w][tid][1];
       }
@@ -2686,7 +2693,7 @@ int launch_conv_halo_split(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
-// conv_ws_split_kernel: one persistent block per CU (ABD_WS=0 restores gemm_nt_bf16_kernel)
+// conv_ws_split_kernel: persistent blocks, one per CU (ABD_WS=0 restores gemm_nt_bf16_kernel)
 int ws_grid() {
   static int n = 0;
   if (n == 0) {
@@ -2701,15 +2708,22 @@ bool ws_on() {
   static const bool on = env_int("ABD_WS", 1) != 0;
   return on;
 }
+// blocks of a launch: conv2 one 8-wave block per CU; conv3 (48 KB of weights) two 8-wave blocks
+int ws_blocks(int N, int Cs) { return (N == 64 && Cs == 64) ? ws_grid() : 2 * ws_grid(); }
 template <int EPI>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
-  if (!ws_on() || a.Cs != 64 || a.N != 64 || a.taps != 4 || a.ksplit > 1 || a.ldb != 256 || a.ldc != 64) return -1;
-  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != ws_grid()) return -1;
-  if ((int64_t)a.Hs * a.Ws * 64 * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
+  if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
+  const int nb = ws_blocks(a.N, a.Cs);
+  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
+  if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
-  static const int pdw = env_int("ABD_WS_PD", 4);
-  if (pdw == 2) conv_ws_split_kernel<EPI, 2><<<dim3(ws_grid()), dim3(kWsT), 0, s>>>(a);
-  else conv_ws_split_kernel<EPI, 4><<<dim3(ws_grid()), dim3(kWsT), 0, s>>>(a);
+  if (a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 32) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else {
+    if (phase >= 0) abd::prof_end(phase, s);
+    return -1;
+  }
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -2917,7 +2931,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
     const bool ws = sp && ws_on();
     a.nblk = bf ? (a.M + kBM - 1) / kBM
-             : ws ? ws_grid()
+             : ws ? ws_blocks(64, 64)
              : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
              : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
@@ -2956,9 +2970,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
-    a.nblk = (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
+    const bool ws3 = sp3 && ws_on();
+    a.nblk = ws3 ? ws_blocks(32, 64) : (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     if (bf3   ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD)
+        : ws3 ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD)
         : sp3 ? launch_nt_bf16<32, EPI_CONV, 32, 3>(a, s, abd::PH_CONV3_FWD)
               : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
       return -1;
@@ -3136,7 +3152,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.part, pa.nblk, 32, G[P_C3B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if (net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
-        : net->precision == ABD_PREC_F32_SPLIT ? launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD)
+        : net->precision == ABD_PREC_F32_SPLIT
+            ? (launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD) == 0
+                   ? 0
+                   : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD))
                                                : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
       return -1;
   }
