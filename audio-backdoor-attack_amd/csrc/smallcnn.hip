@@ -1579,20 +1579,27 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
       }
     };
     f32x16 acc[MI][NJ];
-    auto step = [&](int ks, float4 (&r)[MI][2], const RowInfo& li, int lks) {
-      bf16x8 av[MI][3], bv[NJ][3];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) split3_x8(r[i][0], r[i][1], av[i]);
-      // keep the refill behind the split: hoisted above it, the loads need fresh registers and
-      // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
-      __builtin_amdgcn_sched_barrier(0);
-      load(li, lks, r);  // unconditional: a conditional refill is a phi (copies)
+    // B fragments of a K step (identical for every tile), double-buffered: step ks's MFMAs use
+    // bvs[ks & 1] while the reads for step ks + 1 are in flight (LDS latency off the MFMA path)
+    bf16x8 bvs[2][NJ][3];
+    auto load_b = [&](int ks, bf16x8 (&bv)[NJ][3]) {
       const int kb = ks * 16 + kq;  // k = tap * CS + channel, 16 per step
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
+    };
+    auto step = [&](int ks, float4 (&r)[MI][2], const RowInfo& li, int lks) {
+      bf16x8 av[MI][3];
+      bf16x8 (&bv)[NJ][3] = bvs[ks & 1];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) split3_x8(r[i][0], r[i][1], av[i]);
+      // keep the refill behind the split: hoisted above it, the loads need fresh registers and
+      // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
+      __builtin_amdgcn_sched_barrier(0);
+      load(li, lks, r);  // unconditional: a conditional refill is a phi (copies)
+      load_b((ks + 1) % KS, bvs[(ks + 1) & 1]);
       // term-major: independent accumulator chains between dependent MFMAs
       constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
 #pragma unroll
@@ -1606,6 +1613,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
     RowInfo li = rows_of(r_lo);
 #pragma unroll
     for (int sl = 0; sl < PDW; ++sl) load(li, sl, raw[sl]);
+    load_b(0, bvs[0]);
 #pragma unroll 1
     for (int tile = 0; tile < ntiles; ++tile) {
 #pragma unroll
@@ -2717,7 +2725,10 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
   if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
-  if (a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  static const int cfg = env_int("ABD_WS_CFG", 2);  // conv2 tile / ring / waves-per-block (A/B knob)
+  if (a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16><<<dim3(nb), dim3(1024), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 64 && cfg == 2) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
   else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
   else if (a.N == 64 && a.Cs == 32) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
   else {
