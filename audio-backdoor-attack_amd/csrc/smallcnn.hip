@@ -2156,6 +2156,139 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) 
   }
 }
 
+// conv2 weight gradient on bf16 MFMA with fp32-accurate products (ABD_PREC_F32_SPLIT; round 2).
+// dW[n][t*64 + c] = sum_q dz[q][n] * src[q + off(t)][c]: the reduction index q (positions) is the
+// outer NHWC index of both operands, so the MFMA operands are column reads of row-major images.
+// Per chunk of R output rows of one utterance, dz rows (at the source row stride Ws = Wo + 1, pad
+// column and tail zeroed) and the R + 1 source rows are staged ONCE, split into three exact bf16
+// planes, as row-major LDS images (one 448-B row per position: planes at +0/+128/+256 B, 64 B pad --
+// a 16-bank row step, so the four rows of a transposed read's 32-lane half land on distinct banks),
+// and the fragments are read with ds_read_b64_tr_b16 (gfx950 transpose read: lane i of a 16-lane
+// group receives column i of 4 rows).  Wave w owns tap w: 2 x 2 accumulator tiles (64 n x 64 c),
+// six MFMA terms per 16-position step.  Chunk c + 1's global loads are in flight while chunk c's
+// MFMAs run (registers), then split into the other LDS buffer.  Slabs as conv_wgrad_rows_kernel.
+constexpr int kTrRow = 448;  // bytes per staged position (3 planes x 64 bf16 + pad)
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+template <int R>
+__global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
+  constexpr int NB = 64, CIN = 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int Ws = a.Ws, Wo = a.Wo;
+  const int Qd = ((R * Ws + 15) / 16) * 16;  // dz image rows (16-position steps)
+  const int Qs = Qd + Ws + 1;                // source image rows (tap offsets up to Ws + 1)
+  const int nd4 = Qd * 16, ns4 = Qs * 16;    // float4 slots (16 per position)
+  const int bufb = (Qd + Qs) * kTrRow;
+  const int SLOTS = (nd4 + ns4 + kT - 1) / kT;
+  constexpr int MAXS = 8;  // register staging capacity per thread (checked by the launcher)
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
+  float4 st[MAXS];
+  // global -> registers for chunk c (zeros where the image has no data)
+  auto fetch = [&](int c) {
+    const int b = c / a.cpb, h0 = (c - b * a.cpb) * R;
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) {
+      const int i = threadIdx.x + k * kT;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < SLOTS) {
+        if (i < nd4) {
+          const int q = i >> 4, c4 = i & 15, r = q / Ws, w = q - r * Ws;
+          if (r < R && w < Wo && h0 + r < a.Ho)
+            v = *reinterpret_cast<const float4*>(a.dz + (((int64_t)b * a.Ho + h0 + r) * Wo + w) * NB + 4 * c4);
+        } else if (i < nd4 + ns4) {
+          const int q = (i - nd4) >> 4, c4 = (i - nd4) & 15;
+          if (q < (R + 1) * Ws && h0 + q / Ws < a.Hs)
+            v = *reinterpret_cast<const float4*>(a.src + ((int64_t)b * a.Hs + h0) * Ws * CIN + (int64_t)q * CIN + 4 * c4);
+        }
+      }
+      st[k] = v;
+    }
+  };
+  // registers -> three exact bf16 planes in image buffer `buf`
+  auto put = [&](unsigned char* buf) {
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) {
+      const int i = threadIdx.x + k * kT;
+      if (k < SLOTS && i < nd4 + ns4) {
+        const int row = i < nd4 ? (i >> 4) : Qd + ((i - nd4) >> 4);
+        const int c4 = i & 15;  // nd4 is a multiple of 16
+        f32x2 x[2] = {f32x2{st[k].x, st[k].y}, f32x2{st[k].z, st[k].w}};
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          uint32_t u[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x[h], bf16x2));
+            if (pl < 2) {
+              const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+              x[h] -= back;
+            }
+          }
+          *reinterpret_cast<uint2*>(buf + row * kTrRow + pl * 128 + c4 * 8) = make_uint2(u[0], u[1]);
+        }
+      }
+    }
+  };
+  // transposed fragment of image rows [row0 + 8h, +8) at columns 32 tile + (lane & 31), plane pl
+  const int g = (lane >> 4) & 1, h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto frag = [&](const unsigned char* img, int row0, int tile, int pl) -> bf16x8 {
+    const int col = 32 * tile + 16 * g + 4 * pp;
+    const unsigned char* p = img + (row0 + 8 * h + qq) * kTrRow + pl * 128 + col * 2;
+    const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p));
+    const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p + 4 * kTrRow));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  const int toff = (wave >> 1) * Ws + (wave & 1);  // this wave's tap (dh, dw) as a position offset
+  if (c0 < c1) {
+    fetch(c0);
+    put(lds_tr);
+  }
+  for (int c = c0; c < c1; ++c) {
+    __syncthreads();  // chunk c's images are complete; the other buffer is free
+    const unsigned char* cur = lds_tr + ((c - c0) & 1) * bufb;
+    if (c + 1 < c1) fetch(c + 1);  // in flight while the MFMAs run
+    const unsigned char* dzi = cur;
+    const unsigned char* sri = cur + Qd * kTrRow;
+    for (int q0 = 0; q0 < Qd; q0 += 16) {
+      bf16x8 av[2][3], bv[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          av[t][pl] = frag(dzi, q0, t, pl);
+          bv[t][pl] = frag(sri, q0 + toff, t, pl);
+        }
+      constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
+#pragma unroll
+      for (int term = 0; term < 6; ++term)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
+    }
+    if (c + 1 < c1) put(lds_tr + ((c + 1 - c0) & 1) * bufb);
+  }
+  // slab: D[n][c] of tap `wave`: row n = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col c = 32 j + (lane & 31)
+  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[(int64_t)n * (4 * CIN) + wave * CIN + 32 * j + (lane & 31)] = acc[i][j][r];
+      }
+}
+
 __global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int nslab, int N, int Ktot, int conv_cin,
                                                          float* out) {
   const int64_t total = (int64_t)N * Ktot;
@@ -2623,6 +2756,48 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 // Row-chunk wgrad launch (conv_wgrad_rows_kernel); returns the slab count, -1 on error.
 // R = output rows per chunk (ABD_WGRAD_R<layer> overrides, for tuning); the grid is the
 // resident block count (occupancy API) capped by the slab buffer.
+// conv_wgrad_tr_kernel<2> launch (conv2 shapes: 64 -> 64 channels); -1 when the geometry does not fit
+int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
+                    float* slab, int phase, hipStream_t s) {
+  constexpr int R = 2;
+  if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
+  WGArgs a{};
+  a.dz = dz;
+  a.src = src;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.R = R;
+  a.cpb = (Ho + R - 1) / R;
+  a.nchunks = (int)(B * a.cpb);
+  a.slab = slab;
+  const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
+  if ((Qd + Qs) * 16 > 8 * kT) return -1;  // register staging capacity (MAXS)
+  const size_t lds = 2 * (size_t)(Qd + Qs) * kTrRow;
+  static size_t cached = 0;
+  static int per_cu = 1, n_cu = 256;
+  if (cached != lds) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int dev = 0;
+    ABD_HIP(hipGetDevice(&dev));
+    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R>),
+                                                         kT, lds));
+    per_cu = std::max(1, per_cu);
+    cached = lds;
+  }
+  int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
+  a.per = (a.nchunks + grid - 1) / grid;
+  grid = (a.nchunks + a.per - 1) / a.per;
+  if (phase >= 0) abd::prof_begin(phase, s);
+  conv_wgrad_tr_kernel<R><<<grid, kT, lds, s>>>(a);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return grid;
+}
+
 template <int NB, int CIN>
 int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int R,
                       int max_slabs, float* slab, int phase, hipStream_t s, bool split = false) {
@@ -3191,9 +3366,14 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
-    const int nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
-                                              spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
-                                              kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s, spw);
+    static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
+    int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
+                  ? launch_wgrad_tr(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s)
+                  : -1;
+    if (nsl < 0)
+      nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
+                                      spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
+                                      kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s, spw);
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s, BiasSum{w.part, pa.nblk, 64, G[P_C2B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
