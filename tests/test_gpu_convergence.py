@@ -64,11 +64,12 @@ def fix_random(seed=35):
 _DATA = {}
 
 
-def eval_model(name, dev, source, ref):
+def eval_model(name, dev, source, ref, prec="f32"):
     c = CONV_CFGS[name]
     torch.manual_seed(c["init_seed"])
     m = smallcnn(c["K"], c["lf"])
     m.to(dev)
+    m.set_gemm_precision(prec)   # "f32split": the bench's conv GEMMs (bench.py --gemm-precision default)
     crit = torch.nn.CrossEntropyLoss()
     opt = torch.optim.Adam(m.parameters(), lr=1e-4)
     fix_random()
@@ -110,15 +111,17 @@ def envelope(ref, spread, floor_rel):
 LATER_FLOOR = 5e-4
 
 
+@pytest.mark.parametrize("prec", ["f32", "f32split"])
 @pytest.mark.parametrize("name", list(CONV_CFGS))
-def test_replay_matches_reference_epochs(dev, conv_ref, name):
-    tr, te, m, d = eval_model(name, dev, "torch_cpu", conv_ref)
+def test_replay_matches_reference_epochs(dev, conv_ref, name, prec):
+    """ultrasonic/f32split is the bench's exact geometry and kernels (B = 512, K = 35, 100 x 40)."""
+    tr, te, m, d = eval_model(name, dev, "torch_cpu", conv_ref, prec)
     rtr, rte = conv_ref[f"{name}_train"], conv_ref[f"{name}_test"]
     s_tr, s_te = conv_ref[f"{name}_train_alt"], conv_ref[f"{name}_test_alt"]
     n_train, n_test = CONV_CFGS[name]["n_train"], CONV_CFGS[name]["n_test"]
     n_pois, n_bd = int(d["ind"].sum()), int(d["bt_ind"].sum())
     rel = lambda a, b: np.abs(a - b) / np.maximum(np.abs(b), 1e-12)  # noqa: E731
-    print(f"\n{name}: per-epoch |GPU - reference| / |reference| (train loss, clean loss, bd loss) beside the "
+    print(f"\n{name} [{prec}]: per-epoch |GPU - reference| / |reference| (train loss, clean loss, bd loss) beside the "
           "reference's second fp32 implementation (native conv)")
     for e in range(len(rtr)):
         print(f"  epoch {e + 1:2d}: GPU {rel(tr[e, 0], rtr[e, 0]):.1e} {rel(te[e, 2], rte[e, 2]):.1e} "
@@ -150,9 +153,10 @@ def test_replay_matches_reference_epochs(dev, conv_ref, name):
         assert abs(_digest(v, 21)[1] - ref[1]) <= 1e-2 * abs(ref[1]), k
 
 
+@pytest.mark.parametrize("prec", ["f32", "f32split"])
 @pytest.mark.parametrize("name", list(CONV_CFGS))
-def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name):
-    tr, te, _, _ = eval_model(name, dev, "device", conv_ref)
+def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name, prec):
+    tr, te, _, _ = eval_model(name, dev, "device", conv_ref, prec)
     rte = conv_ref[f"{name}_test"]
     assert tr[-1, 0] < tr[0, 0]                                  # training converges
     assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5, (te[-1], rte[-1])   # clean accuracy (pp)
