@@ -2169,21 +2169,21 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) 
 // MFMAs run (registers), then split into the other LDS buffer.  Slabs as conv_wgrad_rows_kernel.
 constexpr int kTrRow = 448;  // bytes per staged position (3 planes x 64 bf16 + pad)
 typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-template <int R>
+template <int R, int NB>  // NB: output channels (64: conv2, 32: conv3); CIN = 64 input channels
 __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
-  constexpr int NB = 64, CIN = 64;
+  constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int Ws = a.Ws, Wo = a.Wo;
   const int Qd = ((R * Ws + 15) / 16) * 16;  // dz image rows (16-position steps)
   const int Qs = Qd + Ws + 1;                // source image rows (tap offsets up to Ws + 1)
-  const int nd4 = Qd * 16, ns4 = Qs * 16;    // float4 slots (16 per position)
+  const int nd4 = Qd * D4, ns4 = Qs * 16;    // float4 slots (D4 per dz position, 16 per source position)
   const int bufb = (Qd + Qs) * kTrRow;
   const int SLOTS = (nd4 + ns4 + kT - 1) / kT;
   constexpr int MAXS = 8;  // register staging capacity per thread (checked by the launcher)
-  f32x16 acc[2][2];
+  f32x16 acc[NT][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -2199,7 +2199,7 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < SLOTS) {
         if (i < nd4) {
-          const int q = i >> 4, c4 = i & 15, r = q / Ws, w = q - r * Ws;
+          const int q = i / D4, c4 = i % D4, r = q / Ws, w = q - r * Ws;
           if (r < R && w < Wo && h0 + r < a.Ho)
             v = *reinterpret_cast<const float4*>(a.dz + (((int64_t)b * a.Ho + h0 + r) * Wo + w) * NB + 4 * c4);
         } else if (i < nd4 + ns4) {
@@ -2217,8 +2217,8 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
     for (int k = 0; k < MAXS; ++k) {
       const int i = threadIdx.x + k * kT;
       if (k < SLOTS && i < nd4 + ns4) {
-        const int row = i < nd4 ? (i >> 4) : Qd + ((i - nd4) >> 4);
-        const int c4 = i & 15;  // nd4 is a multiple of 16
+        const int row = i < nd4 ? i / D4 : Qd + ((i - nd4) >> 4);
+        const int c4 = i < nd4 ? i % D4 : (i - nd4) & 15;
         f32x2 x[2] = {f32x2{st[k].x, st[k].y}, f32x2{st[k].z, st[k].w}};
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) {
@@ -2257,19 +2257,19 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
     const unsigned char* dzi = cur;
     const unsigned char* sri = cur + Qd * kTrRow;
     for (int q0 = 0; q0 < Qd; q0 += 16) {
-      bf16x8 av[2][3], bv[2][3];
+      bf16x8 av[NT][3], bv[2][3];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          av[t][pl] = frag(dzi, q0, t, pl);
-          bv[t][pl] = frag(sri, q0 + toff, t, pl);
-        }
+        for (int t = 0; t < NT; ++t) av[t][pl] = frag(dzi, q0, t, pl);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) bv[t][pl] = frag(sri, q0 + toff, t, pl);
+      }
       constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
 #pragma unroll
       for (int term = 0; term < 6; ++term)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NT; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
@@ -2279,7 +2279,7 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
   // slab: D[n][c] of tap `wave`: row n = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col c = 32 j + (lane & 31)
   float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -2756,10 +2756,10 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 // Row-chunk wgrad launch (conv_wgrad_rows_kernel); returns the slab count, -1 on error.
 // R = output rows per chunk (ABD_WGRAD_R<layer> overrides, for tuning); the grid is the
 // resident block count (occupancy API) capped by the slab buffer.
-// conv_wgrad_tr_kernel<2> launch (conv2 shapes: 64 -> 64 channels); -1 when the geometry does not fit
+// conv_wgrad_tr_kernel<R, NB> launch (64 input channels); -1 when the geometry does not fit
+template <int R, int NB>
 int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                     float* slab, int phase, hipStream_t s) {
-  constexpr int R = 2;
   if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
   WGArgs a{};
   a.dz = dz;
@@ -2773,17 +2773,17 @@ int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, i
   a.nchunks = (int)(B * a.cpb);
   a.slab = slab;
   const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
-  if ((Qd + Qs) * 16 > 8 * kT) return -1;  // register staging capacity (MAXS)
+  if (Qd * (NB / 4) + Qs * 16 > 8 * kT) return -1;  // register staging capacity (MAXS)
   const size_t lds = 2 * (size_t)(Qd + Qs) * kTrRow;
   static size_t cached = 0;
   static int per_cu = 1, n_cu = 256;
   if (cached != lds) {
-    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R>),
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int dev = 0;
     ABD_HIP(hipGetDevice(&dev));
     ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R>),
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB>),
                                                          kT, lds));
     per_cu = std::max(1, per_cu);
     cached = lds;
@@ -2792,7 +2792,7 @@ int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, i
   a.per = (a.nchunks + grid - 1) / grid;
   grid = (a.nchunks + a.per - 1) / a.per;
   if (phase >= 0) abd::prof_begin(phase, s);
-  conv_wgrad_tr_kernel<R><<<grid, kT, lds, s>>>(a);
+  conv_wgrad_tr_kernel<R, NB><<<grid, kT, lds, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return grid;
@@ -3332,8 +3332,17 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
-    const int nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
-                                              kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s, spw);
+    static const bool trw3 = env_int("ABD_WGRAD_TR", 1) != 0;
+    int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw3 && !spw)
+                  ? (env_int("ABD_WGRAD_TR_R3", 4) == 2
+                         ? launch_wgrad_tr<2, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
+                                                  abd::PH_CONV3_WGRAD, s)
+                         : launch_wgrad_tr<4, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
+                                                  abd::PH_CONV3_WGRAD, s))
+                  : -1;
+    if (nsl < 0)
+      nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
+                                      kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s, spw);
     // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.part, pa.nblk, 32, G[P_C3B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
@@ -3368,7 +3377,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
     int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
-                  ? launch_wgrad_tr(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s)
+                  ? (env_int("ABD_WGRAD_TR_R", 2) == 1
+                         ? launch_wgrad_tr<1, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                                  abd::PH_CONV2_WGRAD, s)
+                         : launch_wgrad_tr<2, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                                  abd::PH_CONV2_WGRAD, s))
                   : -1;
     if (nsl < 0)
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
