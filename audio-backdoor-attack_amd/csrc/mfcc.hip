@@ -574,7 +574,7 @@ __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __re
 
 // =====================================================================================
 // Specialised STFT+mel kernel for the attack geometries (compile-time radix plans).
-//   n_fft 1103 (ultrasonic, Bluestein M = 2304 = 16*16*9), 2048 = 16*16*8 (flowmur, daba),
+//   n_fft 1103 (ultrasonic, Bluestein M = 2304 = 16*12*12), 2048 = 16*16*8 (flowmur, daba),
 //   400 = 16*25 (badnets, jingleback).
 // vs the generic kernel: radix-16/25/9/8 butterflies in registers (2-3 LDS passes instead of
 // 4-6), divisions by compile-time constants, twiddle table in LDS (persistent blocks load it
@@ -749,6 +749,9 @@ __device__ __forceinline__ void dftv_tw_col(f2v* t) {
 template <int N1, int N2>
 __device__ __forceinline__ void dftv_comp(f2v* v);
 
+#ifndef ABD_R12_N1
+#define ABD_R12_N1 4  // radix-12 butterfly as 4 x 3 (ABD_R12_N1=3: 3 x 4)
+#endif
 template <int R>
 struct DftV {
   static __device__ __forceinline__ void run(f2v* v) { dftv<R>(v); }
@@ -760,6 +763,10 @@ struct DftV<8> {
 template <>
 struct DftV<9> {
   static __device__ __forceinline__ void run(f2v* v) { dftv_comp<3, 3>(v); }
+};
+template <>
+struct DftV<12> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<ABD_R12_N1, 12 / ABD_R12_N1>(v); }
 };
 template <>
 struct DftV<16> {
@@ -1673,7 +1680,16 @@ __global__ void __launch_bounds__(kThreads) trig_grad_kernel(const float* __rest
 struct FastPlan {
   int M, N, bluestein, pp, r0, r1;
 };
-constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1, 16, 16}, {2048, 2048, 0, 4, 16, 16}, {400, 400, 0, 13, 16, 25}};
+// Bluestein 2304 = R0 * R1 * R2
+#ifndef ABD_BLUE_R0
+#define ABD_BLUE_R0 16
+#endif
+#ifndef ABD_BLUE_R1
+#define ABD_BLUE_R1 12
+#endif
+constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (ABD_BLUE_R0 * ABD_BLUE_R1);
+constexpr FastPlan kFastPlans[] = {
+    {2304, 1103, 1, 1, kBlueR0, kBlueR1}, {2048, 2048, 0, 4, 16, 16}, {400, 400, 0, 13, 16, 25}};
 
 const FastPlan* find_fast(int M, int N, int blue) {
   for (const auto& f : kFastPlans)
@@ -1716,7 +1732,7 @@ int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const
                   const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
                   hipStream_t s) {
   if (d.M == 2304 && d.N == 1103 && d.bluestein)
-    return launch_fast<2304, 1103, 16, 16, 9, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
+    return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
                                                        queue, s);
   if (d.M == 2048 && d.N == 2048 && !d.bluestein)
     return launch_fast<2048, 2048, 16, 16, 8, 4, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db,
