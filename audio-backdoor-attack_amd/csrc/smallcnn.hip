@@ -1611,8 +1611,14 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
     };
     RowInfo li = rows_of(r_lo);
+    // in step order: the scheduler otherwise issues them last-slot-first, slot 0 becomes the
+    // youngest load on loop entry, and the waitcnt merged at the tile-loop header (entry edge
+    // vs back edge) drains every load in flight at the start of EVERY tile
 #pragma unroll
-    for (int sl = 0; sl < PDW; ++sl) load(li, sl, raw[sl]);
+    for (int sl = 0; sl < PDW; ++sl) {
+      load(li, sl, raw[sl]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     load_b(0, bvs[0]);
 #pragma unroll 1
     for (int tile = 0; tile < ntiles; ++tile) {
@@ -2190,25 +2196,41 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
   float4 st[MAXS];
-  // global -> registers for chunk c (zeros where the image has no data)
+  // Slot geometry is fixed across chunks: slot k of this thread reads dz element (row r, column w,
+  // channels 4 c4) or source element (position q, channels 4 c4) of the chunk, at a byte offset
+  // relative to the chunk's first row (off0) plus h0 rows.  Rows past the utterance's last fall
+  // out of the per-utterance buffer descriptor (zeros); the dz pad column and unused slots take
+  // an out-of-range offset.  nd4 is a multiple of 64, so a slot's operand is wave-uniform.
+  constexpr uint32_t kOOB = 0x80000000u;
+  uint32_t off0[MAXS];
+  bool isdz[MAXS];
+#pragma unroll
+  for (int k = 0; k < MAXS; ++k) {
+    const int i = threadIdx.x + k * kT;
+    isdz[k] = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63) + k * kT < nd4;
+    if (i < nd4) {
+      const int q = i / D4, c4 = i % D4, r = q / Ws, w = q - r * Ws;
+      off0[k] = (r < R && w < Wo) ? (uint32_t)(((r * Wo + w) * NB + 4 * c4) * 4) : kOOB;
+    } else {
+      const int q = (i - nd4) >> 4, c4 = (i - nd4) & 15;
+      off0[k] = (k < SLOTS && i < nd4 + ns4 && q < (R + 1) * Ws) ? (uint32_t)((q * CIN + 4 * c4) * 4) : kOOB;
+    }
+  }
+  // global -> registers for chunk c
   auto fetch = [&](int c) {
     const int b = c / a.cpb, h0 = (c - b * a.cpb) * R;
+    const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.dz) + (int64_t)b * a.Ho * Wo * NB, 0, a.Ho * Wo * NB * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.src) + (int64_t)b * a.Hs * Ws * CIN, 0, a.Hs * Ws * CIN * 4, 0x00020000);
+    const uint32_t hdz = (uint32_t)(h0 * Wo * NB * 4), hsr = (uint32_t)(h0 * Ws * CIN * 4);
 #pragma unroll
     for (int k = 0; k < MAXS; ++k) {
-      const int i = threadIdx.x + k * kT;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < SLOTS) {
-        if (i < nd4) {
-          const int q = i / D4, c4 = i % D4, r = q / Ws, w = q - r * Ws;
-          if (r < R && w < Wo && h0 + r < a.Ho)
-            v = *reinterpret_cast<const float4*>(a.dz + (((int64_t)b * a.Ho + h0 + r) * Wo + w) * NB + 4 * c4);
-        } else if (i < nd4 + ns4) {
-          const int q = (i - nd4) >> 4, c4 = (i - nd4) & 15;
-          if (q < (R + 1) * Ws && h0 + q / Ws < a.Hs)
-            v = *reinterpret_cast<const float4*>(a.src + ((int64_t)b * a.Hs + h0) * Ws * CIN + (int64_t)q * CIN + 4 * c4);
-        }
+        const uint32_t o = off0[k] == kOOB ? kOOB : off0[k] + (isdz[k] ? hdz : hsr);
+        st[k] = __builtin_bit_cast(float4, isdz[k] ? __builtin_amdgcn_raw_buffer_load_b128(rdz, (int)o, 0, 0)
+                                                   : __builtin_amdgcn_raw_buffer_load_b128(rsr, (int)o, 0, 0));
       }
-      st[k] = v;
     }
   };
   // registers -> three exact bf16 planes in image buffer `buf`
