@@ -2175,8 +2175,12 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) 
 // MFMAs run (registers), then split into the other LDS buffer.  Slabs as conv_wgrad_rows_kernel.
 constexpr int kTrRow = 448;  // bytes per staged position (3 planes x 64 bf16 + pad)
 typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-template <int R, int NB>  // NB: output channels (64: conv2, 32: conv3); CIN = 64 input channels
-__global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
+//   NBUF 1: one image buffer (52 KB for conv2: 3 blocks per CU; chunk c + 1 is written
+//   behind a second barrier once every wave has finished reading chunk c; measured equal, and its 3x
+//   slabs cost more in the reduction); NBUF 2 (default, ABD_WGRAD_TR_BUF): double-buffered
+//   (one barrier per chunk, but 104 KB: one block, i.e. one wave per SIMD)
+template <int R, int NB, int NBUF>  // NB: output channels (64: conv2, 32: conv3); CIN = 64 input channels
+__global__ void __launch_bounds__(kT, NBUF == 1 ? 3 : 2) conv_wgrad_tr_kernel(WGArgs a) {
   constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2274,7 +2278,7 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
   }
   for (int c = c0; c < c1; ++c) {
     __syncthreads();  // chunk c's images are complete; the other buffer is free
-    const unsigned char* cur = lds_tr + ((c - c0) & 1) * bufb;
+    const unsigned char* cur = lds_tr + (NBUF == 2 ? ((c - c0) & 1) * bufb : 0);
     if (c + 1 < c1) fetch(c + 1);  // in flight while the MFMAs run
     const unsigned char* dzi = cur;
     const unsigned char* sri = cur + Qd * kTrRow;
@@ -2296,9 +2300,184 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_tr_kernel(WGArgs a) {
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
     }
-    if (c + 1 < c1) put(lds_tr + ((c + 1 - c0) & 1) * bufb);
+    if (c + 1 < c1) {
+      if constexpr (NBUF == 1) __syncthreads();  // every wave is done with chunk c's images
+      put(lds_tr + (NBUF == 2 ? ((c + 1 - c0) & 1) * bufb : 0));
+    }
   }
   // slab: D[n][c] of tap `wave`: row n = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col c = 32 j + (lane & 31)
+  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[(int64_t)n * (4 * CIN) + wave * CIN + 32 * j + (lane & 31)] = acc[i][j][r];
+      }
+}
+
+// Software-pipelined variant of conv_wgrad_tr_kernel (default; ABD_WGRAD_TRP=0 restores the
+// kernel above).  One 4-wave block per CU (the double-buffered images take 104 KB), so a wave has
+// no partner on its SIMD to hide its non-MFMA work: every chunk's staging is moved inside the
+// previous chunk's MFMA stream instead.
+//   * chunk c + 2's global loads are issued at the top of chunk c (two chunks ahead: a whole
+//     chunk of MFMAs covers their latency);
+//   * chunk c + 1's registers are split and written to the other image buffer slot by slot
+//     between chunk c's MFMAs (the MFMA pipe leaves 24 of its 32 cycles to vector issue);
+//   * the next 16-position step's fragments are read after the current step's first term, so the
+//     LDS latency is off the MFMA path and the lgkmcnt range (15) still covers the older reads.
+// NS = Qd / 16 steps and MAXS staging slots are compile-time (checked by the launcher); slots
+// past the images write a trash row (row Qd + Qs of each buffer).  Same sums as the kernel above
+// in the same order: the results are bit-identical.
+#ifndef ABD_TRP_ABL  // ablation bits (measurement builds): 1 no MFMAs, 2 no staging writes, 4 no loads
+#define ABD_TRP_ABL 0
+#endif
+template <int R, int NB, int NS, int MAXS>
+__global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
+  constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4, Qd = 16 * NS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int Ws = a.Ws, Wo = a.Wo;
+  const int Qs = Qd + Ws + 1;
+  const int nd4 = Qd * D4, ns4 = Qs * 16;
+  const int bufb = (Qd + Qs + 1) * kTrRow;
+  constexpr uint32_t kOOB = 0x80000000u;
+  uint32_t off0[MAXS], loff[MAXS];
+  bool isdz[MAXS];
+#pragma unroll
+  for (int k = 0; k < MAXS; ++k) {
+    const int i = threadIdx.x + k * kT;
+    isdz[k] = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63) + k * kT < nd4;
+    int row, c4;
+    if (i < nd4) {
+      const int q = i / D4, r = q / Ws, w = q - r * Ws;
+      c4 = i % D4;
+      row = q;
+      off0[k] = (r < R && w < Wo) ? (uint32_t)(((r * Wo + w) * NB + 4 * c4) * 4) : kOOB;
+    } else {
+      const int q = (i - nd4) >> 4;
+      c4 = (i - nd4) & 15;
+      const bool ok = i < nd4 + ns4;
+      row = ok ? Qd + q : Qd + Qs;  // trash row
+      off0[k] = (ok && q < (R + 1) * Ws) ? (uint32_t)((q * CIN + 4 * c4) * 4) : kOOB;
+    }
+    loff[k] = (uint32_t)(row * kTrRow + c4 * 8);
+  }
+  f32x16 acc[NT][2];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
+  auto fetch = [&](int c, float4 (&st)[MAXS]) {
+    const int b = c / a.cpb, h0 = (c - b * a.cpb) * R;
+    const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.dz) + (int64_t)b * a.Ho * Wo * NB, 0, a.Ho * Wo * NB * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.src) + (int64_t)b * a.Hs * Ws * CIN, 0, a.Hs * Ws * CIN * 4, 0x00020000);
+    const uint32_t hdz = (uint32_t)(h0 * Wo * NB * 4), hsr = (uint32_t)(h0 * Ws * CIN * 4);
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) {
+      if constexpr (ABD_TRP_ABL & 4) {
+        st[k] = make_float4((float)c, 1.f, 2.f, 3.f);
+        continue;
+      }
+      const uint32_t o = off0[k] == kOOB ? kOOB : off0[k] + (isdz[k] ? hdz : hsr);
+      st[k] = __builtin_bit_cast(float4, isdz[k] ? __builtin_amdgcn_raw_buffer_load_b128(rdz, (int)o, 0, 0)
+                                                 : __builtin_amdgcn_raw_buffer_load_b128(rsr, (int)o, 0, 0));
+    }
+  };
+  auto put_slot = [&](int k, const float4& v, unsigned char* buf) {
+    if constexpr (ABD_TRP_ABL & 2) return;
+    f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      uint32_t u[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x[h], bf16x2));
+        if (pl < 2) {
+          const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+          x[h] -= back;
+        }
+      }
+      *reinterpret_cast<uint2*>(buf + loff[k] + pl * 128) = make_uint2(u[0], u[1]);
+    }
+  };
+  const int g = (lane >> 4) & 1, h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto frag = [&](const unsigned char* img, int row0, int tile, int pl) -> bf16x8 {
+    const int col = 32 * tile + 16 * g + 4 * pp;
+    const unsigned char* p = img + (row0 + 8 * h + qq) * kTrRow + pl * 128 + col * 2;
+    const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p));
+    const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p + 4 * kTrRow));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  const int toff = (wave >> 1) * Ws + (wave & 1);
+  struct Frags {
+    bf16x8 av[NT][3], bv[2][3];
+  };
+  auto load_frags = [&](const unsigned char* cur, int s, Frags& F) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) F.av[t][pl] = frag(cur, 16 * s, t, pl);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) F.bv[t][pl] = frag(cur + Qd * kTrRow, 16 * s + toff, t, pl);
+    }
+  };
+  constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
+  auto term = [&](const Frags& F, int tm) {
+    if constexpr (ABD_TRP_ABL & 1) return;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.av[i][TA[tm]], F.bv[j][TB[tm]], acc[i][j], 0, 0, 0);
+  };
+  // chunk c from `cur`; chunk c + 1's registers stP -> `nxt`; chunk c + 2 -> stF
+  auto body = [&](int c, const unsigned char* cur, unsigned char* nxt, const float4 (&stP)[MAXS],
+                  float4 (&stF)[MAXS]) {
+    __syncthreads();  // chunk c's images complete; every wave is done with chunk c - 1 (= nxt)
+    fetch(min(c + 2, c1 - 1), stF);
+    Frags F[2];
+    load_frags(cur, 0, F[0]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      term(F[s & 1], 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // every read of this step's fragments done (they have had a step to land): otherwise the
+      // 24 reads issued next push the older ones past lgkmcnt's range and the waits for terms
+      // 1-5 also wait for most of the new reads
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      if (s + 1 < NS) load_frags(cur, s + 1, F[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int tm = 1; tm < 6; ++tm) {
+        term(F[s & 1], tm);
+#pragma unroll
+        for (int k = 0; k < MAXS; ++k)  // slot k rides on step k % NS, term 1 + (k / NS) % 5
+          if (k % NS == s && 1 + (k / NS) % 5 == tm) put_slot(k, stP[k], nxt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  float4 stA[MAXS], stB[MAXS];
+  unsigned char* buf0 = lds_tr;
+  unsigned char* buf1 = lds_tr + bufb;
+  if (c0 < c1) {
+    fetch(c0, stA);
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) put_slot(k, stA[k], buf0);
+    fetch(min(c0 + 1, c1 - 1), stA);
+  }
+  for (int c = c0; c < c1; c += 2) {
+    body(c, buf0, buf1, stA, stB);
+    if (c + 1 < c1) body(c + 1, buf1, buf0, stB, stA);
+  }
   float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
 #pragma unroll
   for (int i = 0; i < NT; ++i)
@@ -2779,8 +2958,8 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
 // R = output rows per chunk (ABD_WGRAD_R<layer> overrides, for tuning); the grid is the
 // resident block count (occupancy API) capped by the slab buffer.
 // conv_wgrad_tr_kernel<R, NB> launch (64 input channels); -1 when the geometry does not fit
-template <int R, int NB>
-int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
+template <int R, int NB, int NBUF>
+int launch_wgrad_tr_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                     float* slab, int phase, hipStream_t s) {
   if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
   WGArgs a{};
@@ -2796,16 +2975,16 @@ int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, i
   a.slab = slab;
   const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
   if (Qd * (NB / 4) + Qs * 16 > 8 * kT) return -1;  // register staging capacity (MAXS)
-  const size_t lds = 2 * (size_t)(Qd + Qs) * kTrRow;
+  const size_t lds = NBUF * (size_t)(Qd + Qs) * kTrRow;
   static size_t cached = 0;
   static int per_cu = 1, n_cu = 256;
   if (cached != lds) {
-    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB>),
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB, NBUF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int dev = 0;
     ABD_HIP(hipGetDevice(&dev));
     ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB>),
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB, NBUF>),
                                                          kT, lds));
     per_cu = std::max(1, per_cu);
     cached = lds;
@@ -2814,10 +2993,78 @@ int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, i
   a.per = (a.nchunks + grid - 1) / grid;
   grid = (a.nchunks + a.per - 1) / a.per;
   if (phase >= 0) abd::prof_begin(phase, s);
-  conv_wgrad_tr_kernel<R, NB><<<grid, kT, lds, s>>>(a);
+  conv_wgrad_tr_kernel<R, NB, NBUF><<<grid, kT, lds, s>>>(a);
   if (phase >= 0) abd::prof_end(phase, s);
   ABD_LAUNCH_CHECK();
   return grid;
+}
+
+// conv_wgrad_trp_kernel<R, NB, NS, MAXS> launch; -1 when the geometry is not this instantiation's
+template <int R, int NB, int NS, int MAXS>
+int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
+                       float* slab, int phase, hipStream_t s) {
+  if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
+  const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
+  if (Qd != 16 * NS || (Qd * (NB / 4) + Qs * 16 + kT - 1) / kT > MAXS) return -1;
+  WGArgs a{};
+  a.dz = dz;
+  a.src = src;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.R = R;
+  a.cpb = (Ho + R - 1) / R;
+  a.nchunks = (int)(B * a.cpb);
+  a.slab = slab;
+  const size_t lds = 2 * (size_t)(Qd + Qs + 1) * kTrRow;
+  if (lds > 160 * 1024) return -1;
+  auto* kern = &conv_wgrad_trp_kernel<R, NB, NS, MAXS>;
+  static size_t cached = 0;
+  static int per_cu = 1, n_cu = 256;
+  if (cached != lds) {
+    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    int dev = 0;
+    ABD_HIP(hipGetDevice(&dev));
+    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kT, lds));
+    per_cu = std::max(1, per_cu);
+    cached = lds;
+  }
+  int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
+  a.per = (a.nchunks + grid - 1) / grid;
+  grid = (a.nchunks + a.per - 1) / a.per;
+  if (phase >= 0) abd::prof_begin(phase, s);
+  kern<<<grid, kT, lds, s>>>(a);
+  if (phase >= 0) abd::prof_end(phase, s);
+  ABD_LAUNCH_CHECK();
+  return grid;
+}
+
+template <int R, int NB>
+int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
+                    float* slab, int phase, hipStream_t s) {
+  static const bool trp = env_int("ABD_WGRAD_TRP", 1) != 0;
+  if (trp) {
+    int r = -1;
+    // conv2 at W = 40 (Ws = 13): 6-row chunks fill 72 of 80 staged positions (2-row: 24 of 32)
+    static const int r6 = env_int("ABD_WGRAD_TRP_R6", 1);
+    if constexpr (NB == 64) {
+      if (r6) r = launch_wgrad_trp_n<6, NB, 5, 11>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 2, 5>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 8>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 4>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    } else {
+      r = launch_wgrad_trp_n<R, NB, 2, 4>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 6>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 2>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    }
+    if (r >= 0) return r;
+  }
+  static const int nbuf = env_int("ABD_WGRAD_TR_BUF", 2);
+  return nbuf == 2 ? launch_wgrad_tr_n<R, NB, 2>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s)
+                   : launch_wgrad_tr_n<R, NB, 1>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
 }
 
 template <int NB, int CIN>
