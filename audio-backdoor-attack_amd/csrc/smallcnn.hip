@@ -800,6 +800,57 @@ __global__ void bn_sync_bwd_finalize_kernel(const double* sums, int C, const flo
   bcoef[c] = BCoef{g, g * (mdyx * invstd * mean - mdy), -g * mdyx * invstd, 0.0};
 }
 
+// BatchNorm backward statistics of the layer that feeds a 2x2 convolution without padding (BN1 ->
+// pool1 -> conv2, BN2 -> pool2 -> conv3), from that convolution's weight / bias gradients instead
+// of a pass over the activations.  Max-pool routes each pooled gradient dp to one element, whose
+// normalised value is (p - beta) / gamma with p the stored BN+pool output (the conv's input), so
+//   sum dy         = sum_pos dp(pos, c)
+//   sum dy * xhat  = sum_pos dp(pos, c) * (p(pos, c) - beta_c) / gamma_c,
+// and with dp = conv^T(dz) (every output o feeds input o + tap):
+//   sum_pos dp(pos, c)             = sum_{n,t} W[n,c,t] * db[n]      (db = sum_o dz: the bias gradient)
+//   sum_pos dp(pos, c) * p(pos, c) = sum_{n,t} W[n,c,t] * G[n,c,t]   (G: the conv weight gradient)
+// -- a 4 * Cout-term contraction per channel, evaluated in double.  sums != nullptr (SyncBN): this
+// rank's sums go to sums[c], sums[C + c], sums[2C] = count for the all-reduce; otherwise the backward
+// coefficients are written as bn_bwd_finalize_kernel does.
+__global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, const float* G, const float* db, int Cout,
+                                                            int Cin, const float* gamma, const float* beta,
+                                                            const float4* coef, double count, float* dgamma,
+                                                            float* dbeta, BCoef* bcoef, double* sums) {
+  const int c = blockIdx.x;
+  const double b = (double)beta[c];
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < Cout * 4; i += kT) {
+    const int n = i >> 2, t = i & 3;
+    const int64_t e = ((int64_t)n * Cin + c) * 4 + t;
+    const double w = (double)W[e], d = (double)db[n];
+    s1 = fma(w, d, s1);
+    s2 = fma(w, fma(-b, d, (double)G[e]), s2);
+  }
+  __shared__ double red[2][kT / kWave];
+  s1 = abd::wave_sum_d(s1);
+  s2 = abd::wave_sum_d(s2);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s1;
+    red[1][threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s1 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    s2 = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (double)gamma[c];
+    dgamma[c] = (float)s2;
+    dbeta[c] = (float)s1;
+    if (sums) {
+      sums[c] = s1;
+      sums[Cin + c] = s2;
+      if (c == 0) sums[2 * Cin] = count;
+      return;
+    }
+    const double g = (double)gamma[c] * (double)coef[c].y, mdy = s1 / count, mdyx = s2 / count;
+    const double mean = (double)coef[c].x, invstd = (double)coef[c].y;
+    bcoef[c] = BCoef{g, g * (mdyx * invstd * mean - mdy), -g * mdyx * invstd, 0.0};
+  }
+}
+
 // sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
 // conv1 mode (gw != nullptr): columns j*64 + c, j < 4 -> conv1.weight (c,1,kh,kw) = gw[c*4 + j], j = 4 -> gb[c]
 // sum_{i < n} p[i * stride] in index order (the same rounding as a serial loop), loads issued
@@ -2774,6 +2825,15 @@ struct abd_cnn {
   int max_batch;
   int64_t off[P_COUNT + 1];
   int precision = ABD_PREC_F32;  // ABD_PREC_BF16: conv2/conv3 fwd + dgrad on bf16 MFMA
+  // weight-gradient side stream (created on first use): conv3 / conv2 weight gradients run there,
+  // concurrently with the data-gradient chain of the caller's stream, joined before return
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  ~abd_cnn() {
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
+  }
 };
 
 namespace {
@@ -2783,6 +2843,7 @@ struct Work {
   float *dp3, *da, *dz3, *dp2, *dz2, *dp1;
   float *w2f, *w2d, *w3f, *w3d, *f1t;
   float* part;
+  float *partb3, *partb2;  // BN3 / BN2 backward-apply bias partials (read by the side stream's slab reduction)
   float* slab;
   float* slab2;   // group sums of slab (hierarchical reduce) / fc1 split-K partials
   float4* coef;   // 3 x 64
@@ -2849,6 +2910,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   w.bcoef = reinterpret_cast<BCoef*>(take(3 * 64 * sizeof(BCoef)));
   w.mask1 = reinterpret_cast<uint8_t*>(take((size_t)B * g.flat));
   w.mask2 = reinterpret_cast<uint8_t*>(take((size_t)B * 128));
+  w.partb3 = F(4096LL * 64);  // grid_for caps the apply grids at 4096 blocks
+  w.partb2 = F(4096LL * 64);
   w.bytes = off;
   return w;
 }
@@ -3327,6 +3390,21 @@ int bn_bwd_finalize(const BnSync& y, int point, const float* part, int nblk, int
   return 0;
 }
 
+// backward coefficients of the BatchNorm feeding a 2x2 conv, from the conv's gradients
+// (bn_bwd_derived_kernel); W, G: (Cout, Cin, 2, 2), db: (Cout)
+int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, const float* db, int Cout, int Cin,
+                  double count, const float* gamma, const float* beta, const float4* coef, float* dgamma, float* dbeta,
+                  BCoef* bcoef, hipStream_t s) {
+  double* buf = y.on() ? y.buf + (int64_t)point * ABD_BN_SYNC_STRIDE : nullptr;
+  bn_bwd_derived_kernel<<<Cin, kT, 0, s>>>(W, G, db, Cout, Cin, gamma, beta, coef, count, dgamma, dbeta, bcoef, buf);
+  ABD_LAUNCH_CHECK();
+  if (!y.on()) return 0;
+  if (sync_point(y, point, Cin)) return -1;
+  bn_sync_bwd_finalize_kernel<<<1, 64, 0, s>>>(buf, Cin, gamma, coef, bcoef);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
@@ -3506,8 +3584,47 @@ int loss_and_metrics(abd_cnn* net, const Work& w, const Params& P, const int64_t
   return 0;
 }
 
+// BN2 / BN1 backward statistics derived from the next conv's weight / bias gradients
+// (bn_bwd_derived_kernel); ABD_BN_BWD_STATS=0 restores the passes over the activations
+// (bn_pool_bwd_stats_kernel / conv1_bwd_stats_kernel).
+bool bn_bwd_derived_on() {
+  static const bool on = env_int("ABD_BN_BWD_STATS", 1) != 0;
+  return on;
+}
+// Stream for the conv weight gradients: they depend only on dz and the stored forward activations and
+// feed nothing but the final gradient buffer, so they run on a side stream of the net while the data-
+// gradient chain (dgrad -> BN backward -> ...) continues on the caller's stream; backward() joins it
+// before returning.  Opt-in (ABD_WGRAD_SIDE=1): measured 2-4 % slower per step than one stream
+// (the weight-gradient and data-gradient kernels compete for the same CUs; with the derived BN
+// statistics the chain joins right after each data gradient anyway).
+hipStream_t wgrad_stream(abd_cnn* net, hipStream_t s) {
+  static const bool on = env_int("ABD_WGRAD_SIDE", 0) != 0;
+  if (!on) return s;
+  if (!net->side) {
+    hipStream_t t = nullptr;
+    if (hipStreamCreateWithFlags(&t, hipStreamNonBlocking) != hipSuccess) return s;
+    if (hipEventCreateWithFlags(&net->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(t);
+      return s;
+    }
+    net->side = t;
+  }
+  return net->side;
+}
+
+// everything enqueued on `from` so far happens before what is enqueued on `to` next
+int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
+  if (from == to) return 0;
+  ABD_HIP(hipEventRecord(ev, from));
+  ABD_HIP(hipStreamWaitEvent(to, ev, 0));
+  return 0;
+}
+
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{}) {
+  const hipStream_t sw = wgrad_stream(net, s);
+  const bool derive = bn_bwd_derived_on();
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -3595,32 +3712,34 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       return -1;
     pa.bcoef = w.bcoef + 128;
     pa.dz = w.dz3;
+    pa.part = w.partb3;
     pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 32 / 4);
     abd::prof_begin(abd::PH_BN3_BWD, s);
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
+    if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw3 = env_int("ABD_WGRAD_TR", 1) != 0;
     int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw3 && !spw)
                   ? (env_int("ABD_WGRAD_TR_R3", 4) == 2
                          ? launch_wgrad_tr<2, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
-                                                  abd::PH_CONV3_WGRAD, s)
+                                                  abd::PH_CONV3_WGRAD, sw)
                          : launch_wgrad_tr<4, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
-                                                  abd::PH_CONV3_WGRAD, s))
+                                                  abd::PH_CONV3_WGRAD, sw))
                   : -1;
     if (nsl < 0)
       nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
-                                      kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, s, spw);
+                                      kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, sw, spw);
     // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
-    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.part, pa.nblk, 32, G[P_C3B]})) return -1;
+    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], sw, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
-    if (net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
+    if ((net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
         : net->precision == ABD_PREC_F32_SPLIT
             ? (launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD) == 0
                    ? 0
                    : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD))
-                                               : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
+                                               : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)))
       return -1;
   }
   // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
@@ -3631,35 +3750,44 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.dp = w.dp2;
     pa.part = w.part;
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
-    bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
-    ABD_LAUNCH_CHECK();
-    if (bn_bwd_finalize(sy, 4, w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64, G[P_BN2W],
-                        G[P_BN2B], w.bcoef + 64, s))
-      return -1;
+    if (derive) {  // conv3's weight / bias gradients (side stream) are final here
+      if (stream_dep(net->ev_join, sw, s) ||
+          bn_bwd_derive(sy, 4, P.p[P_C3W], G[P_C3W], G[P_C3B], 32, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W],
+                        P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s))
+        return -1;
+    } else {
+      bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+      ABD_LAUNCH_CHECK();
+      if (bn_bwd_finalize(sy, 4, w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64, G[P_BN2W],
+                          G[P_BN2B], w.bcoef + 64, s))
+        return -1;
+    }
     pa.bcoef = w.bcoef + 64;
     pa.dz = w.dz2;
+    pa.part = w.partb2;
     pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 64 / 4);
     abd::prof_begin(abd::PH_BN2_BWD, s);
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
+    if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
     int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
                   ? (env_int("ABD_WGRAD_TR_R", 2) == 1
                          ? launch_wgrad_tr<1, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                  abd::PH_CONV2_WGRAD, s)
+                                                  abd::PH_CONV2_WGRAD, sw)
                          : launch_wgrad_tr<2, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                  abd::PH_CONV2_WGRAD, s))
+                                                  abd::PH_CONV2_WGRAD, sw))
                   : -1;
     if (nsl < 0)
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
                                       spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
-                                      kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, s, spw);
-    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s, BiasSum{w.part, pa.nblk, 64, G[P_C2B]})) return -1;
+                                      kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, sw, spw);
+    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], sw, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]})) return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
-    if (net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
+    if ((net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
         : net->precision == ABD_PREC_F32_SPLIT
             ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
                : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0 ? 0
@@ -3669,7 +3797,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                   : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD))
         : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
         : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
-                                    : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
+                                    : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)))
       return -1;
   }
   // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
@@ -3685,11 +3813,18 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.B = (int)B;
     c1.nblk = (int)nblk_conv1(g, B);
     c1.rows = c1_rows();
-    conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
-    ABD_LAUNCH_CHECK();
-    if (bn_bwd_finalize(sy, 5, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef, G[P_BN1W],
-                        G[P_BN1B], w.bcoef, s))
-      return -1;
+    if (derive) {  // conv2's weight / bias gradients (side stream) are final here
+      if (stream_dep(net->ev_join, sw, s) ||
+          bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
+                        P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s))
+        return -1;
+    } else {
+      conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+      ABD_LAUNCH_CHECK();
+      if (bn_bwd_finalize(sy, 5, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef, G[P_BN1W],
+                          G[P_BN1B], w.bcoef, s))
+        return -1;
+    }
     c1.bcoef = w.bcoef;
     abd::prof_begin(abd::PH_CONV1_BWD, s);
     if (g.W1 % 3 == 0)
@@ -3702,7 +3837,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, nullptr, G[P_C1W], G[P_C1B]);
     ABD_LAUNCH_CHECK();
   }
-  return 0;
+  return stream_dep(net->ev_join, sw, s);
 }
 
 DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask, int64_t cols) {
