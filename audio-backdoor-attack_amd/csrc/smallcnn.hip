@@ -2864,6 +2864,20 @@ int env_int(const char* name, int dflt) {
 int c1_rows() { return std::max(1, std::min(kR1, env_int("ABD_C1_ROWS", 8))); }
 int64_t nchunks_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + c1_rows() - 1) / c1_rows()); }
 int64_t nblk_conv1(const Geo& g, int64_t B) { return std::min<int64_t>(nchunks_conv1(g, B), env_int("ABD_C1_CAP", 2048)); }
+// resident blocks of conv1_wgrad_kernel over the device (ABD_C1W_CAP overrides)
+template <bool FULL>
+int64_t c1w_blocks() {
+  static int64_t n = 0;
+  if (n == 0) {
+    int dev = 0, cu = 256, per = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&conv1_wgrad_kernel<FULL>),
+                                                       kT, 0);
+    n = env_int("ABD_C1W_CAP", 0) > 0 ? env_int("ABD_C1W_CAP", 0) : (int64_t)cu * std::max(1, per);
+  }
+  return n;
+}
 
 Work layout(const abd_cnn* net, int64_t B, char* base) {
   const Geo& g = net->g;
@@ -3826,6 +3840,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
         return -1;
     }
     c1.bcoef = w.bcoef;
+    // one resident round: the grid-stride chunk loop otherwise runs a second, partial round of
+    // blocks (occupancy 5 blocks/CU < the 8 of the stats kernels' 2048-block grid)
+    c1.nblk = (int)std::min<int64_t>(c1.nblk, g.W1 % 3 == 0 ? c1w_blocks<true>() : c1w_blocks<false>());
     abd::prof_begin(abd::PH_CONV1_BWD, s);
     if (g.W1 % 3 == 0)
       conv1_wgrad_kernel<true><<<c1.nblk, kT, 0, s>>>(c1);
