@@ -3237,8 +3237,13 @@ bool ws_on() {
   static const bool on = env_int("ABD_WS", 1) != 0;
   return on;
 }
-// blocks of a launch: conv2 one 8-wave block per CU; conv3 (48 KB of weights) two 8-wave blocks
-int ws_blocks(int N, int Cs) { return (N == 64 && Cs == 64) ? ws_grid() : 2 * ws_grid(); }
+// blocks of a launch: one 8-wave block per CU.  conv3 (48 KB of weights, 132-190 VGPRs) also fits
+// only one 8-wave block per CU, so ABD_WS3_MULT=2 runs its second block per CU as a second round
+// (measured: conv3 fwd 0.037 -> 0.033 ms, dgrad 0.031 -> 0.026 ms with one)
+int ws_blocks(int N, int Cs) {
+  static const int m3 = std::max(1, env_int("ABD_WS3_MULT", 1));
+  return (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
+}
 template <int EPI>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
