@@ -147,8 +147,31 @@ struct BCoef {
   double g, A, B, pad;
 };
 
+#ifndef ABD_C1_DD
+#define ABD_C1_DD 0
+#endif
 __device__ __forceinline__ float bn_dx(float dy, float r, float4 /*cf*/, const BCoef& bc) {
   return (float)fma(bc.B, (double)r, fma(bc.g, (double)dy, bc.A));
+}
+
+// bn_dx in float-float arithmetic: each double coefficient carried as hi + lo fp32 parts (the
+// parts' sum is the double to ~2^-48), dx = (B_hi r + g_hi dy + A_hi) + (B_lo r + g_lo dy + A_lo).
+// The batch-mean terms keep their double precision (no systematic bias for the cancelling
+// weight-gradient sums); what remains is the per-element fp32 rounding the double path also has
+// at its final store.  Channel pairs on v_pk_fma_f32 (conv1_wgrad_kernel); ABD_C1_DD=1 builds the
+// double-precision evaluation instead.
+struct BCoefF {
+  float gh, gl, Ah, Al, Bh, Bl;
+};
+__device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
+  BCoefF f;
+  f.gh = (float)c.g;
+  f.gl = (float)(c.g - (double)f.gh);
+  f.Ah = (float)c.A;
+  f.Al = (float)(c.A - (double)f.Ah);
+  f.Bh = (float)c.B;
+  f.Bl = (float)(c.B - (double)f.Bh);
+  return f;
 }
 
 struct C1Args {
@@ -391,6 +414,18 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     bb[q] = cf.w;
     bc[q] = a.bcoef[c0 + q];
   }
+#if !ABD_C1_DD
+  c1f2 fgh, fgl, fAh, fAl, fBh, fBl;  // float-float coefficients of the channel pair
+  {
+    const BCoefF f0 = bcoef_ff(bc[0]), f1 = bcoef_ff(bc[1]);
+    fgh = c1f2{f0.gh, f1.gh};
+    fgl = c1f2{f0.gl, f1.gl};
+    fAh = c1f2{f0.Ah, f1.Ah};
+    fAl = c1f2{f0.Al, f1.Al};
+    fBh = c1f2{f0.Bh, f1.Bh};
+    fBl = c1f2{f0.Bl, f1.Bl};
+  }
+#endif
   const int NW = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (dy = 0 there)
   static_assert(CPT == 2, "one packed channel pair per thread");
   c1f2 kp[5], vp[5];
@@ -449,8 +484,20 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
       for (int j = 0; j < 3; ++j) {
         if (j >= nw) continue;
         c1f2 dz;
+#if ABD_C1_DD
         dz.x = r[0][j] > 0.0f ? bn_dx(j == jm[0] ? dd[0] : 0.0f, r[0][j], float4{}, bc[0]) : 0.0f;
         dz.y = r[1][j] > 0.0f ? bn_dx(j == jm[1] ? dd[1] : 0.0f, r[1][j], float4{}, bc[1]) : 0.0f;
+#else
+        {
+          const c1f2 dy = c1f2{j == jm[0] ? dd[0] : 0.0f, j == jm[1] ? dd[1] : 0.0f};
+          const c1f2 rr = c1f2{r[0][j], r[1][j]};
+          const c1f2 hi = __builtin_elementwise_fma(fBh, rr, __builtin_elementwise_fma(fgh, dy, fAh));
+          const c1f2 lo = __builtin_elementwise_fma(fBl, rr, __builtin_elementwise_fma(fgl, dy, fAl));
+          const c1f2 v = hi + lo;
+          dz.x = rr.x > 0.0f ? v.x : 0.0f;
+          dz.y = rr.y > 0.0f ? v.y : 0.0f;
+        }
+#endif
         vp[0] = __builtin_elementwise_fma(dz, c1f2{xv[0][j], xv[0][j]}, vp[0]);
         vp[1] = __builtin_elementwise_fma(dz, c1f2{xv[0][j + 1], xv[0][j + 1]}, vp[1]);
         vp[2] = __builtin_elementwise_fma(dz, c1f2{xv[1][j], xv[1][j]}, vp[2]);
