@@ -174,6 +174,37 @@ __device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
   return f;
 }
 
+// weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets), fc1^T
+struct PrepArgs {
+  const float *c2w, *c3w, *f1w;
+  int flat;
+  float *w2f, *w2d, *w3f, *w3d, *f1t;
+};
+
+__device__ __forceinline__ void prep_weights_body(const PrepArgs& a, int bx, int nb) {
+  const int64_t n2 = 64 * 64 * 4, n3 = 32 * 64 * 4, nf = 128LL * a.flat;
+  const int64_t total = n2 + n3 + nf;
+  for (int64_t e = bx * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)nb * kT) {
+    if (e < n2) {
+      const int co = (int)(e / 256), ci = (int)(e / 4 % 64), t = (int)(e % 4);
+      const float v = a.c2w[e];
+      a.w2f[(co * 4 + t) * 64 + ci] = v;
+      a.w2d[(ci * 4 + t) * 64 + co] = v;
+    } else if (e < n2 + n3) {
+      const int64_t f = e - n2;
+      const int co = (int)(f / 256), ci = (int)(f / 4 % 64), t = (int)(f % 4);
+      const float v = a.c3w[f];
+      a.w3f[(co * 4 + t) * 64 + ci] = v;
+      a.w3d[(ci * 4 + t) * 32 + co] = v;
+    } else {
+      const int64_t f = e - n2 - n3;
+      const int j = (int)(f / a.flat), k = (int)(f % a.flat);
+      a.f1t[(int64_t)k * 128 + j] = a.f1w[f];
+    }
+  }
+}
+__global__ void __launch_bounds__(kT) prep_weights_kernel(PrepArgs a) { prep_weights_body(a, blockIdx.x, gridDim.x); }
+
 struct C1Args {
   const float* x;   // (B, H0, W0)
   const float* w;   // conv1.weight (64,1,2,2)
@@ -188,6 +219,8 @@ struct C1Args {
   int B;
   int rows;  // conv1 rows per chunk (<= kR1)
   int coef_bstride;  // 0: one BN1 coefficient set; 64: per utterance (coef + b*64)
+  PrepArgs prep;     // conv1_stats_kernel: blocks [0, nprep) repack the weights
+  int nprep;
 };
 
 // Stage x rows [h0, h0+kR1] of utterance b into LDS.
@@ -264,12 +297,17 @@ __device__ __forceinline__ float4 c1_coef_col(const float4* coef, int c0, int co
 // forward stats: sum / sumsq of relu(conv1) per channel
 __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
+  if ((int)blockIdx.x < a.nprep) {
+    prep_weights_body(a.prep, blockIdx.x, a.nprep);
+    return;
+  }
+  const int bid = (int)blockIdx.x - a.nprep;
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
   const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
   const C1W k = c1_weights(a, c0);
   float v[2][4] = {};
-  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+  for (int chunk = bid; chunk < nchunks; chunk += a.nblk) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
@@ -293,7 +331,7 @@ __global__ void __launch_bounds__(kT) conv1_stats_kernel(C1Args a) {
     }
     __syncthreads();  // xs is restaged by the next chunk
   }
-  cgroup_partials<2>(v, 64, a.part, a.nblk, blockIdx.x);
+  cgroup_partials<2>(v, 64, a.part, a.nblk, bid);
 }
 
 // first maximum of bn(r) over a (1,3) window, per channel: returns the slot index 0..2
@@ -859,20 +897,26 @@ __global__ void bn_sync_bwd_finalize_kernel(const double* sums, int C, const flo
 // -- a 4 * Cout-term contraction per channel, evaluated in double.  sums != nullptr (SyncBN): this
 // rank's sums go to sums[c], sums[C + c], sums[2C] = count for the all-reduce; otherwise the backward
 // coefficients are written as bn_bwd_finalize_kernel does.
-__global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, const float* G, const float* db, int Cout,
-                                                            int Cin, const float* gamma, const float* beta,
-                                                            const float4* coef, double count, float* dgamma,
-                                                            float* dbeta, BCoef* bcoef, double* sums) {
-  const int c = blockIdx.x;
-  const double b = (double)beta[c];
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < Cout * 4; i += kT) {
-    const int n = i >> 2, t = i & 3;
-    const int64_t e = ((int64_t)n * Cin + c) * 4 + t;
-    const double w = (double)W[e], d = (double)db[n];
-    s1 = fma(w, d, s1);
-    s2 = fma(w, fma(-b, d, (double)G[e]), s2);
+// sum_{i < n} p[i * stride] in index order (the same rounding as a serial loop), loads issued
+// 8 at a time so a thread keeps 8 HBM reads in flight
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ p, int64_t stride, int n) {
+  float v = 0.0f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = p[(int64_t)(i + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += t[j];
   }
+  for (; i < n; ++i) v += p[(int64_t)i * stride];
+  return v;
+}
+
+// block-reduce this thread's (s1, s2) share of channel c and write its BN backward outputs
+__device__ __forceinline__ void bn_bwd_derived_finish(int c, double s1, double s2, int Cin, const float* gamma,
+                                                      const float4* coef, double count, float* dgamma, float* dbeta,
+                                                      BCoef* bcoef, double* sums) {
   __shared__ double red[2][kT / kWave];
   s1 = abd::wave_sum_d(s1);
   s2 = abd::wave_sum_d(s2);
@@ -898,24 +942,59 @@ __global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, cons
   }
 }
 
-// sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
-// conv1 mode (gw != nullptr): columns j*64 + c, j < 4 -> conv1.weight (c,1,kh,kw) = gw[c*4 + j], j = 4 -> gb[c]
-// sum_{i < n} p[i * stride] in index order (the same rounding as a serial loop), loads issued
-// 8 at a time so a thread keeps 8 HBM reads in flight
-__device__ __forceinline__ float ordered_sum(const float* __restrict__ p, int64_t stride, int n) {
-  float v = 0.0f;
-  int i = 0;
-  for (; i + 8 <= n; i += 8) {
-    float t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = p[(int64_t)(i + j) * stride];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v += t[j];
+__global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, const float* G, const float* db, int Cout,
+                                                            int Cin, const float* gamma, const float* beta,
+                                                            const float4* coef, double count, float* dgamma,
+                                                            float* dbeta, BCoef* bcoef, double* sums) {
+  const int c = blockIdx.x;
+  const double b = (double)beta[c];
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < Cout * 4; i += kT) {
+    const int n = i >> 2, t = i & 3;
+    const int64_t e = ((int64_t)n * Cin + c) * 4 + t;
+    const double w = (double)W[e], d = (double)db[n];
+    s1 = fma(w, d, s1);
+    s2 = fma(w, fma(-b, d, (double)G[e]), s2);
   }
-  for (; i < n; ++i) v += p[(int64_t)i * stride];
-  return v;
+  bn_bwd_derived_finish(c, s1, s2, Cin, gamma, coef, count, dgamma, dbeta, bcoef, sums);
 }
 
+// The next BatchNorm's derivation fused into the conv weight gradient's last slab reduction
+// (slab_reduce_kernel with conv_cin = Cin): block c reduces the Cout * 4 entries of input channel c
+// (the same ordered_sum, so the gradient is bit-identical), stores them, and contracts them with the
+// conv weights as bn_bwd_derived_kernel does.  db (the conv bias gradient) is final before this launch.
+struct DeriveArgs {
+  const float* W;
+  const float* db;
+  const float* gamma;
+  const float* beta;
+  const float4* coef;
+  double count;
+  float* dgamma;
+  float* dbeta;
+  BCoef* bcoef;
+};
+__global__ void __launch_bounds__(kT) slab_reduce_derive_kernel(const float* slab, int nslab, int Cout, int Ktot,
+                                                                int Cin, float* out, DeriveArgs d) {
+  const int c = blockIdx.x;
+  const int64_t total = (int64_t)Cout * Ktot;
+  const double b = (double)d.beta[c];
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < Cout * 4; i += kT) {
+    const int n = i >> 2, t = i & 3;
+    const float gv = ordered_sum(slab + (int64_t)n * Ktot + t * Cin + c, total, nslab);
+    const int64_t o = ((int64_t)n * Cin + c) * 4 + t;
+    out[o] = gv;
+    const double w = (double)d.W[o], dbn = (double)d.db[n];
+    s1 = fma(w, dbn, s1);
+    s2 = fma(w, fma(-b, dbn, (double)gv), s2);
+  }
+  bn_bwd_derived_finish(c, s1, s2, Cin, d.gamma, d.coef, d.count, d.dgamma, d.dbeta, d.bcoef, nullptr);
+}
+
+
+// sum of nv partial columns: out[j][c] = sum_i part[(j*C + c)*nblk + i]
+// conv1 mode (gw != nullptr): columns j*64 + c, j < 4 -> conv1.weight (c,1,kh,kw) = gw[c*4 + j], j = 4 -> gb[c]
 __device__ __forceinline__ void partial_sum_body(const float* part, int nblk, float* out, float* gw, float* gb,
                                                  int col) {
   double s = 0.0;
@@ -2603,32 +2682,6 @@ __global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int 
   }
 }
 
-// weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets)
-__global__ void __launch_bounds__(kT) prep_weights_kernel(const float* c2w, const float* c3w, const float* f1w,
-                                                          int flat, float* w2f, float* w2d, float* w3f, float* w3d,
-                                                          float* f1t) {
-  const int64_t n2 = 64 * 64 * 4, n3 = 32 * 64 * 4, nf = 128LL * flat;
-  const int64_t total = n2 + n3 + nf;
-  for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    if (e < n2) {
-      const int co = (int)(e / 256), ci = (int)(e / 4 % 64), t = (int)(e % 4);
-      const float v = c2w[e];
-      w2f[(co * 4 + t) * 64 + ci] = v;
-      w2d[(ci * 4 + t) * 64 + co] = v;
-    } else if (e < n2 + n3) {
-      const int64_t f = e - n2;
-      const int co = (int)(f / 256), ci = (int)(f / 4 % 64), t = (int)(f % 4);
-      const float v = c3w[f];
-      w3f[(co * 4 + t) * 64 + ci] = v;
-      w3d[(ci * 4 + t) * 32 + co] = v;
-    } else {
-      const int64_t f = e - n2 - n3;
-      const int j = (int)(f / flat), k = (int)(f % flat);
-      f1t[(int64_t)k * 128 + j] = f1w[f];
-    }
-  }
-}
-
 // ------------------------------------------------------------------ fc2 + loss + metrics
 struct LossArgs {
   const float* d2;   // (B,128)
@@ -2688,7 +2741,7 @@ __global__ void __launch_bounds__(kT) fc2_loss_kernel(LossArgs a) {
 }
 
 // one block: deterministic batch reduction -> metrics (loss mean as double bits, counts)
-__global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B, int64_t* metrics) {
+__device__ __forceinline__ void metrics_body(const float* rowinfo, int B, int64_t* metrics) {
   double s = 0.0;
   long long c = 0, p = 0, h = 0;
   for (int i = threadIdx.x; i < B; i += kT) {
@@ -2721,6 +2774,9 @@ __global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B
     metrics[4] += rc[2][0];
     metrics[5] += 1;
   }
+}
+__global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B, int64_t* metrics) {
+  metrics_body(rowinfo, B, metrics);
 }
 
 // fc2 data gradient through dropout2/ReLU: da = (dz . W2) * scale2 * [d2 > 0]
@@ -2769,15 +2825,21 @@ __global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const f
 
 // fc2_wgrad_kernel and fc2_bwd_kernel in one launch (independent: both only read dz and d2):
 // blocks [0, nw) run two 128-thread (k, split) groups each, the rest fc2_bwd's grid-stride loop
+// metrics != nullptr: the last block reduces the loss kernel's per-row flags into the counters
 __global__ void __launch_bounds__(kT) fc2_grads_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
                                                        int rows, int nsplit, float* part, float scale2, float* da,
-                                                       int nw) {
+                                                       int nw, const float* rowinfo, int64_t* metrics) {
+  const int nb = (int)gridDim.x - (metrics ? 1 : 0);
+  if (metrics && (int)blockIdx.x == nb) {
+    metrics_body(rowinfo, B, metrics);
+    return;
+  }
   if ((int)blockIdx.x < nw) {
     const int pr = (int)blockIdx.x * 2 + (int)(threadIdx.x >> 7);
     if (pr < K * nsplit) fc2_wgrad_body(dz, d2, B, K, rows, part, pr % K, pr / K, threadIdx.x & 127);
     return;
   }
-  fc2_bwd_body(dz, d2, w2, B, K, scale2, da, (int)blockIdx.x - nw, (int)gridDim.x - nw);
+  fc2_bwd_body(dz, d2, w2, B, K, scale2, da, (int)blockIdx.x - nw, nb - nw);
 }
 
 __device__ __forceinline__ void fc2_wgrad_reduce_body(const float* part, int nsplit, int K, float* gw, float* gb, int e) {
@@ -2986,6 +3048,11 @@ Params params_of(const abd_cnn* net, const float* flat) {
   for (int i = 0; i < P_COUNT; ++i) r.p[i] = flat + net->off[i];
   return r;
 }
+
+PrepArgs prep_args(const Params& P, const Work& w, const Geo& g) {
+  return PrepArgs{P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t};
+}
+unsigned prep_blocks(const Geo& g) { return (unsigned)grid_for(64 * 256 + 32 * 256 + 128LL * g.flat); }
 
 PoolArgs pool_args(const Geo& g, int layer, int64_t B) {
   PoolArgs a{};
@@ -3374,8 +3441,10 @@ int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
+// dv != nullptr (conv weight gradients): the final reduction also derives the BatchNorm feeding the
+// conv (slab_reduce_derive_kernel)
 int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s,
-                 BiasSum bias = BiasSum{}) {
+                 BiasSum bias = BiasSum{}, const DeriveArgs* dv = nullptr) {
   const int64_t total = (int64_t)N * Ktot;
   const float* src = w.slab;
   int n = nsl;
@@ -3393,7 +3462,10 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
     src = w.slab2;
     n = G;
   }
-  slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out);
+  if (dv != nullptr && conv_cin > 0)
+    slab_reduce_derive_kernel<<<conv_cin, kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, *dv);
+  else
+    slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out);
   ABD_LAUNCH_CHECK();
   return 0;
 }
@@ -3474,7 +3546,8 @@ int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, co
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
-            int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{}) {
+            int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{},
+            const PrepArgs* prep = nullptr) {
   // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
   // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
@@ -3508,8 +3581,13 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     c1.coef = inst_coef;
     c1.coef_bstride = 64;
   } else if (train) {
+    // prep != nullptr: the first nprep blocks do the weight repacks (prep_weights_body) instead
+    if (prep) {
+      c1.prep = *prep;
+      c1.nprep = (int)std::min<unsigned>(prep_blocks(g), 256u);
+    }
     abd::prof_begin(abd::PH_CONV1_STATS, s);
-    conv1_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
+    conv1_stats_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
     abd::prof_end(abd::PH_CONV1_STATS, s);
     ABD_LAUNCH_CHECK();
     if (bn_fwd_finalize(sy, 0, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B], rmu[0],
@@ -3688,9 +3766,12 @@ int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
 }
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
-             const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{}) {
+             const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
+             int64_t* metrics = nullptr) {
   const hipStream_t sw = wgrad_stream(net, s);
   const bool derive = bn_bwd_derived_on();
+  // derived in the weight gradients' last reduction; SyncBN all-reduces the sums first (separate kernel)
+  const bool derive_fused = derive && !sy.on();
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -3701,8 +3782,8 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     const int rows = (int)((B + kFc2Split - 1) / kFc2Split);
     // two launches instead of four: [fc2 weight-grad partials | da] then [their reduction | fc1 bias]
     const int nw = (g.K * kFc2Split + 1) / 2;
-    fc2_grads_kernel<<<(unsigned)(nw + grid_for(B * 128)), kT, 0, s>>>(w.dz, w.d2, P.p[P_F2W], (int)B, g.K, rows,
-                                                                       kFc2Split, w.slab2, s2, w.da, nw);
+    fc2_grads_kernel<<<(unsigned)(nw + grid_for(B * 128) + (metrics ? 1 : 0)), kT, 0, s>>>(
+        w.dz, w.d2, P.p[P_F2W], (int)B, g.K, rows, kFc2Split, w.slab2, s2, w.da, nw, w.rowinfo, metrics);
     fc2_reduce_colsum_kernel<<<(unsigned)(128 + (g.K * 129 + kT - 1) / kT), kT, 0, s>>>(
         w.slab2, kFc2Split, g.K, G[P_F2W], G[P_F2B], w.da, (int)B, 128, G[P_F1B]);
   }
@@ -3798,7 +3879,12 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
                                       kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, sw, spw);
     // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
-    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], sw, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]})) return -1;
+    // BN2's backward coefficients come out of the same final reduction (derive_fused)
+    const DeriveArgs dv2{P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
+                         G[P_BN2W], G[P_BN2B], w.bcoef + 64};
+    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], sw, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
+                                derive_fused ? &dv2 : nullptr))
+      return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     if ((net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
         : net->precision == ABD_PREC_F32_SPLIT
@@ -3818,8 +3904,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
     if (derive) {  // conv3's weight / bias gradients (side stream) are final here
       if (stream_dep(net->ev_join, sw, s) ||
-          bn_bwd_derive(sy, 4, P.p[P_C3W], G[P_C3W], G[P_C3B], 32, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W],
-                        P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s))
+          (!derive_fused &&
+           bn_bwd_derive(sy, 4, P.p[P_C3W], G[P_C3W], G[P_C3B], 32, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W],
+                         P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s)))
         return -1;
     } else {
       bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
@@ -3850,7 +3937,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
                                       spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
                                       kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, sw, spw);
-    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], sw, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]})) return -1;
+    const DeriveArgs dv1{P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
+                         G[P_BN1W], G[P_BN1B], w.bcoef};
+    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], sw, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]},
+                                derive_fused ? &dv1 : nullptr))
+      return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if ((net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
@@ -3881,8 +3972,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.rows = c1_rows();
     if (derive) {  // conv2's weight / bias gradients (side stream) are final here
       if (stream_dep(net->ev_join, sw, s) ||
-          bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
-                        P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s))
+          (!derive_fused &&
+           bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
+                         P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s)))
         return -1;
     } else {
       conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
@@ -4002,16 +4094,16 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Geo& g = net->g;
   Params P = params_of(net, a->params);
-  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
-      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
-  ABD_LAUNCH_CHECK();
+  // the weight repacks ride on conv1_stats_kernel's launch (forward(..., prep))
+  const PrepArgs prep = prep_args(P, w, g);
   DropArgs d1 = make_drop(a, 1, w.mask1, g.flat), d2 = make_drop(a, 2, w.mask2, 128);
   const BnSync sy = bn_sync_of(a);
-  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy))
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep))
     return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
-  if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, a->metrics, s)) return -1;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy)) return -1;
+  // the metrics reduction rides on backward()'s fc2 gradient launch
+  if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics)) return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
@@ -4032,8 +4124,7 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Geo& g = net->g;
   Params P = params_of(net, a->params);
-  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
-      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  prep_weights_kernel<<<prep_blocks(g), kT, 0, s>>>(prep_args(P, w, g));
   ABD_LAUNCH_CHECK();
   DropArgs d1{}, d2{};
   if (train_mode) {
@@ -4092,8 +4183,7 @@ int abd_smallcnn_eval(abd_cnn* net, const float* x, int64_t batch, const float* 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Geo& g = net->g;
   Params P = params_of(net, params);
-  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
-      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  prep_weights_kernel<<<prep_blocks(g), kT, 0, s>>>(prep_args(P, w, g));
   ABD_LAUNCH_CHECK();
   DropArgs off{};
   if (forward(net, w, P, x, batch, running, nullptr, false, off, off, s)) return -1;
@@ -4124,8 +4214,7 @@ int abd_smallcnn_forward_per_utterance(abd_cnn* net, const float* x, int64_t bat
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Geo& g = net->g;
   Params P = params_of(net, params);
-  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
-      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  prep_weights_kernel<<<prep_blocks(g), kT, 0, s>>>(prep_args(P, w, g));
   ABD_LAUNCH_CHECK();
   abd_train_args a{};
   a.seed = seed;
@@ -4161,8 +4250,7 @@ int abd_smallcnn_input_grad(abd_cnn* net, const float* x, int64_t batch, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Geo& g = net->g;
   Params P = params_of(net, params);
-  prep_weights_kernel<<<grid_for(64 * 256 + 32 * 256 + 128LL * g.flat), kT, 0, s>>>(
-      P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t);
+  prep_weights_kernel<<<prep_blocks(g), kT, 0, s>>>(prep_args(P, w, g));
   ABD_LAUNCH_CHECK();
   DropArgs off{};
   if (forward(net, w, P, x, B, running, nullptr, false, off, off, s)) return -1;
