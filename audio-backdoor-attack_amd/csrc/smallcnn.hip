@@ -221,6 +221,7 @@ struct C1Args {
   int coef_bstride;  // 0: one BN1 coefficient set; 64: per utterance (coef + b*64)
   PrepArgs prep;     // conv1_stats_kernel: blocks [0, nprep) repack the weights
   int nprep;
+  const float* gamma;  // conv1_stats_fold_kernel: BN1 weight (the sign picks max or min per window)
 };
 
 // Stage x rows [h0, h0+kR1] of utterance b into LDS.
@@ -385,6 +386,72 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
     }
     __syncthreads();  // xs is restaged by the next chunk
   }
+}
+
+// Training forward of layer 1 with BN1 folded into conv2 (train step, f32split weight-stationary
+// conv2): ONE pass computes relu(conv1) everywhere, BN1's batch statistics, and per pool1 window
+// the element the pool will select, m = max r (gamma >= 0) or min r (gamma < 0).  For either sign of
+// alpha = gamma * invstd, max_j fl(alpha r_j + beta') = fl(alpha m + beta') (fl is monotone), so
+// p1 = alpha m + beta' once the statistics are known; conv2 consumes m with alpha folded into its
+// weights and beta' into its bias (NTArgs::fold), its weight gradient is corrected the same way
+// (slab_reduce_kernel fold), and conv1_bn_pool_kernel's second conv1 pass disappears.  p1's buffer
+// holds m.  Blocks [0, nprep) repack the weights (prep_weights_body) as in conv1_stats_kernel.
+__global__ void __launch_bounds__(kT) conv1_stats_fold_kernel(C1Args a) {
+  __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
+  if ((int)blockIdx.x < a.nprep) {
+    prep_weights_body(a.prep, blockIdx.x, a.nprep);
+    return;
+  }
+  const int bid = (int)blockIdx.x - a.nprep;
+  const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
+  const int nchunks = a.B * nbh;
+  const int c0 = (threadIdx.x & 15) * 4, pl = threadIdx.x >> 4;
+  const C1W k = c1_weights(a, c0);
+  bool neg[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) neg[q] = a.gamma[c0 + q] < 0.0f;
+  const int NW = (a.g.W1 + 2) / 3;  // windows incl. a partial trailing one (statistics only)
+  const int NWp = a.g.W1p;
+  float v[2][4] = {};
+  for (int chunk = bid; chunk < nchunks; chunk += a.nblk) {
+    const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
+    stage_x(a, b, h0, xs);
+    const int rows = min(a.rows, a.g.H1 - h0);
+    int hl = pl / NW, wo = pl - hl * NW;  // (hl, wo) of idx, stepped without dividing by NW
+    for (int idx = pl; idx < rows * NW; idx += 16, wo += 16) {
+      while (wo >= NW) {
+        wo -= NW;
+        ++hl;
+      }
+      const int w = 3 * wo;
+      const int nw = min(3, a.g.W1 - w);
+      float rr[3][4];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 r = c1_at(xs, a.g.W0, hl, w + j, k);
+        const bool in = j < nw;  // positions past W1 (trailing partial window) contribute nothing
+        rr[j][0] = in ? r.x : 0.0f;
+        rr[j][1] = in ? r.y : 0.0f;
+        rr[j][2] = in ? r.z : 0.0f;
+        rr[j][3] = in ? r.w : 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[0][q] += rr[j][q];
+          v[1][q] = fmaf(rr[j][q], rr[j][q], v[1][q]);
+        }
+      }
+      if (wo < NWp) {  // a real pool1 window (nw == 3)
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = neg[q] ? fminf(fminf(rr[0][q], rr[1][q]), rr[2][q]) : fmaxf(fmaxf(rr[0][q], rr[1][q]), rr[2][q]);
+        *reinterpret_cast<float4*>(a.p1 + (((int64_t)b * a.g.H1 + h0 + hl) * NWp + wo) * 64 + c0) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    __syncthreads();  // xs is restaged by the next chunk
+  }
+  cgroup_partials<2>(v, 64, a.part, a.nblk, bid);
 }
 
 // backward stats: s1 = sum dy, s2 = sum dy * xhat over pool1 argmax positions
@@ -912,6 +979,11 @@ __device__ __forceinline__ float ordered_sum(const float* __restrict__ p, int64_
   for (; i < n; ++i) v += p[(int64_t)i * stride];
   return v;
 }
+// fold != nullptr (conv weight gradient over the folded source m, conv1_stats_fold_kernel): the gradient
+// w.r.t. the conv's true input alpha m + beta' is alpha_ci G_m + beta'_ci db[n] (db: the bias gradient)
+__device__ __forceinline__ float unfold_wgrad(float gm, const float4* fold, const float* db, int n, int ci) {
+  return fold ? (float)fma((double)fold[ci].z, (double)gm, (double)fold[ci].w * (double)db[n]) : gm;
+}
 
 // block-reduce this thread's (s1, s2) share of channel c and write its BN backward outputs
 __device__ __forceinline__ void bn_bwd_derived_finish(int c, double s1, double s2, int Cin, const float* gamma,
@@ -964,6 +1036,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, cons
 // (the same ordered_sum, so the gradient is bit-identical), stores them, and contracts them with the
 // conv weights as bn_bwd_derived_kernel does.  db (the conv bias gradient) is final before this launch.
 struct DeriveArgs {
+  const float4* fold;  // the weight gradient's source is folded (unfold_wgrad)
   const float* W;
   const float* db;
   const float* gamma;
@@ -982,7 +1055,7 @@ __global__ void __launch_bounds__(kT) slab_reduce_derive_kernel(const float* sla
   double s1 = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < Cout * 4; i += kT) {
     const int n = i >> 2, t = i & 3;
-    const float gv = ordered_sum(slab + (int64_t)n * Ktot + t * Cin + c, total, nslab);
+    const float gv = unfold_wgrad(ordered_sum(slab + (int64_t)n * Ktot + t * Cin + c, total, nslab), d.fold, d.db, n, c);
     const int64_t o = ((int64_t)n * Cin + c) * 4 + t;
     out[o] = gv;
     const double w = (double)d.W[o], dbn = (double)d.db[n];
@@ -1246,6 +1319,10 @@ struct NTArgs {
   int nblk;
   DropArgs drop;  // EPI_FC1 (dropout2 on relu(fc1)), EPI_DROPGRAD (dropout1 mask)
   int ksplit;     // EPI_PARTIAL: K chunks split over blockIdx.z, raw sums to out[z][M][ldc]
+  // conv_ws_split_kernel, EPI_CONV: the source holds m with src = alpha_ci m + beta'_ci (BN coefficient
+  // float4 (mean, invstd, alpha, beta') per input channel): alpha folded into the weights, the
+  // beta' terms into the bias (conv1_stats_fold_kernel)
+  const float4* fold;
 };
 
 constexpr int kBM = 128, kKC = 32;
@@ -1682,12 +1759,33 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   static_assert(KS % PDW == 0, "a tile's K steps must be a whole number of ring turns");
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3][N * LD];
   __shared__ float red[WPB][N][2];
+  __shared__ float bfold[N];
+  static_assert((N * (K / 8)) % (WPB * 64) == 0 && (K / 8) <= 64, "fold: whole lane groups per weight row");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // ---- weights -> three exact bf16 planes, [plane][n][k] with k = tap * CS + channel
   for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
     const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
-    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
-    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    if (EPI == EPI_CONV && a.fold != nullptr) {  // w * alpha_ci, rounded once; bias b_n + sum_k w beta'_ci
+      const int ci = k8 % CS;
+      const float wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      double bs = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bs = fma((double)wv[i], (double)a.fold[ci + i].w, bs);
+      // the K / 8 chunks of row n are K / 8 consecutive lanes (N * K / 8 is a multiple of the block)
+#pragma unroll
+      for (int o = K / 16; o > 0; o >>= 1) bs += __shfl_xor(bs, o, 64);
+      if (idx % (K / 8) == 0) bfold[n] = (float)(bs + (double)a.bias[n]);
+      lo.x *= a.fold[ci].z;
+      lo.y *= a.fold[ci + 1].z;
+      lo.z *= a.fold[ci + 2].z;
+      lo.w *= a.fold[ci + 3].z;
+      hi.x *= a.fold[ci + 4].z;
+      hi.y *= a.fold[ci + 5].z;
+      hi.z *= a.fold[ci + 6].z;
+      hi.w *= a.fold[ci + 7].z;
+    }
     bf16x8 pl[3];
     split3_x8(lo, hi, pl);
 #pragma unroll
@@ -1710,7 +1808,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   for (int j = 0; j < NJ; ++j) {
     st[j][0] = st[j][1] = 0.0f;
     bias[j] = 0.0f;
-    if constexpr (EPI == EPI_CONV) bias[j] = a.bias[32 * j + (lane & 31)];
+    if constexpr (EPI == EPI_CONV) bias[j] = a.fold != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
   }
   // One continuous stream of K steps over all of this wave's tiles (KS steps per TR-row tile):
   // the A loads run PDW steps ahead ACROSS tile boundaries, so the pipeline never drains at a
@@ -2668,14 +2766,14 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
 }
 
 __global__ void __launch_bounds__(kT) slab_reduce_kernel(const float* slab, int nslab, int N, int Ktot, int conv_cin,
-                                                         float* out) {
+                                                         float* out, const float4* fold, const float* fold_db) {
   const int64_t total = (int64_t)N * Ktot;
   for (int64_t e = blockIdx.x * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
     const float s = ordered_sum(slab + e, total, nslab);
     const int n = (int)(e / Ktot), k = (int)(e % Ktot);
     if (conv_cin > 0) {
       const int t = k / conv_cin, ci = k % conv_cin;
-      out[((int64_t)n * conv_cin + ci) * 4 + t] = s;
+      out[((int64_t)n * conv_cin + ci) * 4 + t] = unfold_wgrad(s, fold, fold_db, n, ci);
     } else {
       out[e] = s;
     }
@@ -3443,8 +3541,9 @@ int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
 
 // dv != nullptr (conv weight gradients): the final reduction also derives the BatchNorm feeding the
 // conv (slab_reduce_derive_kernel)
+// fold (conv2 under the BN1 fold): the gradient is unfolded with the bias gradient bias.out
 int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s,
-                 BiasSum bias = BiasSum{}, const DeriveArgs* dv = nullptr) {
+                 BiasSum bias = BiasSum{}, const DeriveArgs* dv = nullptr, const float4* fold = nullptr) {
   const int64_t total = (int64_t)N * Ktot;
   const float* src = w.slab;
   int n = nsl;
@@ -3465,7 +3564,7 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
   if (dv != nullptr && conv_cin > 0)
     slab_reduce_derive_kernel<<<conv_cin, kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, *dv);
   else
-    slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out);
+    slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, fold, bias.out);
   ABD_LAUNCH_CHECK();
   return 0;
 }
@@ -3547,7 +3646,7 @@ int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, co
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
             int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{},
-            const PrepArgs* prep = nullptr) {
+            const PrepArgs* prep = nullptr, bool fold1 = false) {
   // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
   // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
@@ -3587,7 +3686,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
       c1.nprep = (int)std::min<unsigned>(prep_blocks(g), 256u);
     }
     abd::prof_begin(abd::PH_CONV1_STATS, s);
-    conv1_stats_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
+    if (fold1) {
+      c1.gamma = P.p[P_BN1W];
+      conv1_stats_fold_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
+    } else {
+      conv1_stats_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
+    }
     abd::prof_end(abd::PH_CONV1_STATS, s);
     ABD_LAUNCH_CHECK();
     if (bn_fwd_finalize(sy, 0, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B], rmu[0],
@@ -3597,10 +3701,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN1W], P.p[P_BN1B], rm[0], rv[0], 64, w.coef);
   }
   ABD_LAUNCH_CHECK();
-  abd::prof_begin(abd::PH_CONV1_POOL, s);
+  if (!fold1) {
+    abd::prof_begin(abd::PH_CONV1_POOL, s);
     conv1_bn_pool_kernel<<<(unsigned)nchunks_conv1(g, B), kT, 0, s>>>(c1);  // no partials: one chunk per block
     abd::prof_end(abd::PH_CONV1_POOL, s);
-  ABD_LAUNCH_CHECK();
+    ABD_LAUNCH_CHECK();
+  }
   // ---- layer 2: conv2 (MFMA) + relu + stats -> BN2 -> pool2
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
@@ -3612,6 +3718,9 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
              : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
              : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
+    // p1 holds m under the BN1 fold: only the weight-stationary split kernel applies it (bn1_fold_ok)
+    ABD_CHECK(!fold1 || ws, ABD_E_UNSUPPORTED, "BN1 fold needs the weight-stationary conv2 kernel");
+    if (fold1) a.fold = w.coef;
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
            : ws ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD)
@@ -3735,6 +3844,14 @@ bool bn_bwd_derived_on() {
   static const bool on = env_int("ABD_BN_BWD_STATS", 1) != 0;
   return on;
 }
+
+// The train step folds BN1 into conv2 (conv1_stats_fold_kernel; ABD_BN1_FOLD=0 restores the separate
+// conv1_bn_pool pass) when conv2's forward runs on the weight-stationary split kernel.
+bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
+  static const bool on = env_int("ABD_BN1_FOLD", 1) != 0;
+  return on && net->precision == ABD_PREC_F32_SPLIT && ws_on() && split_mi() == 1 &&
+         (int64_t)g.H1 * g.W1p * 64 * 4 * B < 0x7ffffff0LL;
+}
 // Stream for the conv weight gradients: they depend only on dz and the stored forward activations and
 // feed nothing but the final gradient buffer, so they run on a side stream of the net while the data-
 // gradient chain (dgrad -> BN backward -> ...) continues on the caller's stream; backward() joins it
@@ -3767,7 +3884,8 @@ int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
-             int64_t* metrics = nullptr) {
+             int64_t* metrics = nullptr, bool fold1 = false) {
+  // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   const hipStream_t sw = wgrad_stream(net, s);
   const bool derive = bn_bwd_derived_on();
   // derived in the weight gradients' last reduction; SyncBN all-reduces the sums first (separate kernel)
@@ -3880,7 +3998,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                       kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, sw, spw);
     // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
     // BN2's backward coefficients come out of the same final reduction (derive_fused)
-    const DeriveArgs dv2{P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
+    const DeriveArgs dv2{nullptr, P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
                          G[P_BN2W], G[P_BN2B], w.bcoef + 64};
     if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], sw, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
                                 derive_fused ? &dv2 : nullptr))
@@ -3937,10 +4055,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
                                       spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
                                       kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, sw, spw);
-    const DeriveArgs dv1{P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
+    const DeriveArgs dv1{fold1 ? w.coef : nullptr, P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
                          G[P_BN1W], G[P_BN1B], w.bcoef};
     if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], sw, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]},
-                                derive_fused ? &dv1 : nullptr))
+                                derive_fused ? &dv1 : nullptr, fold1 ? w.coef : nullptr))
       return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
@@ -4065,6 +4183,10 @@ size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch) {
   return layout(net, batch, nullptr).bytes;
 }
 
+int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch) {
+  return (net && batch >= 2 && bn1_fold_ok(net, net->g, batch)) ? 1 : 0;
+}
+
 int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name) {
   if (!net || !name) return -1;
   char* base = reinterpret_cast<char*>(static_cast<uintptr_t>(4096));  // any non-null base: offsets only
@@ -4096,14 +4218,16 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   Params P = params_of(net, a->params);
   // the weight repacks ride on conv1_stats_kernel's launch (forward(..., prep))
   const PrepArgs prep = prep_args(P, w, g);
+  const bool fold1 = bn1_fold_ok(net, g, B);
   DropArgs d1 = make_drop(a, 1, w.mask1, g.flat), d2 = make_drop(a, 2, w.mask2, 128);
   const BnSync sy = bn_sync_of(a);
-  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep))
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep,
+              fold1))
     return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
   // the metrics reduction rides on backward()'s fc2 gradient launch
   if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics)) return -1;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1)) return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);

@@ -27,8 +27,10 @@ def ws_view(eng, ws, B, name, shape, dtype=torch.float32):
     return ws[off:off + n].view(dtype).view(*shape).cpu().numpy()
 
 
+@pytest.mark.parametrize("prec", ["f32", "f32split"])
 @pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 48)])
-def test_every_buffer_matches_oracle(shape):
+def test_every_buffer_matches_oracle(shape, prec):
+    """prec 'f32split' also covers the train step's BN1 fold into conv2 (conv1_stats_fold_kernel)."""
     assert torch.cuda.is_available()
     abd_amd.load_library()
     dev = torch.device("cuda", 0)
@@ -38,7 +40,7 @@ def test_every_buffer_matches_oracle(shape):
     st = make_state(H, W, K, lf, seed=3000 + H + W + K)
     m = M.smallcnn(K, lf)
     m.load_state_dict({k: torch.tensor(v) for k, v in st.items()})
-    m = m.to(dev).train()
+    m = m.to(dev).train().set_gemm_precision(prec)
     r = np.random.Generator(np.random.PCG64(H * W + B))
     x = mfcc_like(r, B, H, W)
     y = r.integers(0, K, B).astype(np.int64)
@@ -76,11 +78,16 @@ def test_every_buffer_matches_oracle(shape):
         ("dz2", rec["dz2"], nhwc, (B, g["H2"], g["W2"], 64), 1e-5),
         ("dp1", rec["dp1"], nhwc, (B, g["H1p"], g["W1p"], 64), 1e-5),
     ]
+    # f32split train step: BN1 folded into conv2, p1's buffer holds the pool-selected relu(conv1) m
+    folded = L.lib().abd_smallcnn_bn1_folded(eng.h, B) == 1
+    coef1 = ws_view(eng, ws, B, "coef", (3, 64, 4))[0]
     report = {}
     for name, ref, tf, shp, tol in checks:
         got = ws_view(eng, ws, B, name, shp)
+        if name == "p1" and folded:  # p1 = alpha * m + beta' (what conv2's folded weights / bias apply)
+            got = got.astype(np.float64) * coef1[:, 2] + coef1[:, 3]
         refv = tf(ref) if tf else ref
         report[name] = nrel(got, refv)
-    print(shape, "replayed decisions", replayed, {k: f"{v:.1e}" for k, v in report.items()})
+    print(shape, prec, "folded" if folded else "", "replayed decisions", replayed, {k: f"{v:.1e}" for k, v in report.items()})
     for name, ref, tf, shp, tol in checks:
         assert report[name] < tol, (name, report[name])
