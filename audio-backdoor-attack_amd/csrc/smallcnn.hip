@@ -396,6 +396,8 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
 // weights and beta' into its bias (NTArgs::fold), its weight gradient is corrected the same way
 // (slab_reduce_kernel fold), and conv1_bn_pool_kernel's second conv1 pass disappears.  p1's buffer
 // holds m.  Blocks [0, nprep) repack the weights (prep_weights_body) as in conv1_stats_kernel.
+// forward() caps the chunk grid at the kernel's residency (73 VGPRs: 6 blocks per CU), so the chunks
+// run in one round (a 64-VGPR build for 8 blocks per CU spills and measured the same)
 __global__ void __launch_bounds__(kT) conv1_stats_fold_kernel(C1Args a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   if ((int)blockIdx.x < a.nprep) {
@@ -3071,6 +3073,19 @@ int env_int(const char* name, int dflt) {
 int c1_rows() { return std::max(1, std::min(kR1, env_int("ABD_C1_ROWS", 8))); }
 int64_t nchunks_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + c1_rows() - 1) / c1_rows()); }
 int64_t nblk_conv1(const Geo& g, int64_t B) { return std::min<int64_t>(nchunks_conv1(g, B), env_int("ABD_C1_CAP", 2048)); }
+// resident blocks of conv1_stats_fold_kernel over the device
+int64_t c1f_blocks() {
+  static int64_t n = 0;
+  if (n == 0) {
+    int dev = 0, cu = 256, per = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&conv1_stats_fold_kernel),
+                                                       kT, 0);
+    n = (int64_t)cu * std::max(1, per);
+  }
+  return n;
+}
 // resident blocks of conv1_wgrad_kernel over the device (ABD_C1W_CAP overrides)
 template <bool FULL>
 int64_t c1w_blocks() {
@@ -3688,6 +3703,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     abd::prof_begin(abd::PH_CONV1_STATS, s);
     if (fold1) {
       c1.gamma = P.p[P_BN1W];
+      c1.nblk = (int)std::min<int64_t>(c1.nblk, c1f_blocks());  // one resident round
       conv1_stats_fold_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
     } else {
       conv1_stats_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
