@@ -1325,6 +1325,13 @@ struct NTArgs {
   // float4 (mean, invstd, alpha, beta') per input channel): alpha folded into the weights, the
   // beta' terms into the bias (conv1_stats_fold_kernel)
   const float4* fold;
+  // gemm_nt_kernel, EPI_DROPGRAD (fc1 data gradient): part != nullptr also forms BN3's backward sums
+  // sum dy and sum dy * xhat, xhat = (p3d / scale - beta) / gamma over the stored dropout output p3d
+  // (dropped elements have dy = 0), one partial pair per block; bias = beta, bn_period = columns per
+  // channel (a multiple of NB)
+  const float* bnp;
+  const float* bn_gamma;
+  int bn_period;
 };
 
 constexpr int kBM = 128, kKC = 32;
@@ -1456,6 +1463,15 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
     const bool cok = col < a.N;
     float bias = 0.0f;
     if constexpr (EPI == EPI_CONV || EPI == EPI_FC1) bias = cok ? a.bias[col] : 0.0f;
+    float bnb = 0.0f, bngi = 0.0f, inv_scale = 0.0f;  // EPI_DROPGRAD + BN3 sums
+    if constexpr (EPI == EPI_DROPGRAD) {
+      if (a.part != nullptr) {
+        const int ch = n0 / a.bn_period;
+        bnb = a.bias[ch];
+        bngi = 1.0f / a.bn_gamma[ch];
+        inv_scale = 1.0f / a.drop.scale;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1474,6 +1490,10 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
       } else if constexpr (EPI == EPI_DROPGRAD) {
         const bool k = a.drop.mask_in[oi] != 0;
         v = v * (k ? a.drop.scale : 0.0f);
+        if (a.part != nullptr) {
+          st[j][0] += v;
+          st[j][1] = fmaf(v, (a.bnp[oi] * inv_scale - bnb) * bngi, st[j][1]);
+        }
       }
       a.out[oi] = v;
     }
@@ -1501,6 +1521,28 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
       }
       a.part[((int64_t)0 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s0;
       a.part[((int64_t)1 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s1;
+    }
+  }
+  if constexpr (EPI == EPI_DROPGRAD && NJ == 1) {
+    if (a.part == nullptr) return;
+    // every column of the block belongs to one BN3 channel: one partial pair per block
+    float* red = As;
+    const float s0 = abd::wave_sum(st[0][0]), s1 = abd::wave_sum(st[0][1]);
+    if (lane == 0) {
+      red[wave * 2] = s0;
+      red[wave * 2 + 1] = s1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float t0 = 0.0f, t1 = 0.0f;
+      for (int w = 0; w < kT / kWave; ++w) {
+        t0 += red[w * 2];
+        t1 += red[w * 2 + 1];
+      }
+      const int cpb = a.bn_period / NB, ch = n0 / a.bn_period, C = a.N / a.bn_period;
+      const int slot = blockIdx.x * cpb + (int)(blockIdx.y % cpb), nb = gridDim.x * cpb;
+      a.part[((int64_t)0 * C + ch) * nb + slot] = t0;
+      a.part[((int64_t)1 * C + ch) * nb + slot] = t1;
     }
   }
 }
@@ -3904,6 +3946,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   const hipStream_t sw = wgrad_stream(net, s);
   const bool derive = bn_bwd_derived_on();
+  int bn3_parts = 0;  // > 0: BN3 backward partials from the fc1 data-gradient epilogue
   // derived in the weight gradients' last reduction; SyncBN all-reduces the sums first (separate kernel)
   const bool derive_fused = derive && !sy.on();
   const Geo& g = net->g;
@@ -3966,6 +4009,17 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     a.ldc = g.flat;
     a.drop = drop1;
     a.drop.mask_in = drop1.enabled ? w.mask1 : nullptr;
+    // BN3's backward sums in this epilogue (32-column tiles within one channel)
+    static const bool bn3f = env_int("ABD_BN3_FUSED", 1) != 0;
+    const int per3 = g.flat / 32;  // columns per BN3 channel (flatten order c, h, w)
+    if (bn3f && drop1.enabled && per3 % 32 == 0 && env_int("ABD_FC1D_NB", 32) == 32) {
+      a.part = w.part;
+      a.bias = P.p[P_BN3B];
+      a.bn_gamma = P.p[P_BN3W];
+      a.bnp = w.p3d;
+      a.bn_period = per3;
+      bn3_parts = ((a.M + kBM - 1) / kBM) * (per3 / 32);
+    }
     // 32-column tiles: M = B rows is short (4 row tiles at B = 512), so 128-column tiles leave
     // most CUs idle (96 blocks); ABD_FC1D_NB=128 restores them
     static const bool nb128 = env_int("ABD_FC1D_NB", 32) == 128;
@@ -3985,9 +4039,13 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.coef = w.coef + 128;
     pa.dp = w.dp3;
     pa.part = w.part;
-    pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32 / 4);
-    bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
-    ABD_LAUNCH_CHECK();
+    if (bn3_parts > 0) {  // partials from the fc1 data-gradient epilogue
+      pa.nblk = bn3_parts;
+    } else {
+      pa.nblk = grid_for(B * pa.Ho * pa.Wo * 32 / 4);
+      bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
+      ABD_LAUNCH_CHECK();
+    }
     if (bn_bwd_finalize(sy, 3, w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128, G[P_BN3W],
                         G[P_BN3B], w.bcoef + 128, s))
       return -1;
