@@ -62,3 +62,35 @@ def test_bn_backward_sums_from_conv_gradients(H0, W0, K):
         # direct: the BN weight / bias gradients are exactly these sums (oracle bn_backward)
         np.testing.assert_allclose(sdy, grads[f"bn{i}.bias"], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(sdyx, grads[f"bn{i}.weight"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("H0,W0,K", [(20, 40, 10), (17, 12, 5)])
+def test_bn1_fold_identities(H0, W0, K):
+    """The train step's BN1 fold (csrc/smallcnn.hip conv1_stats_fold_kernel, conv_ws_split_kernel
+    fold, unfold_wgrad): pool1 of BN1's output equals alpha * m + beta' with m the window's max
+    relu(conv1) for gamma >= 0 and its min for gamma < 0; conv2 over m with w * alpha and
+    b + sum w * beta' equals conv2 over p1; the weight gradient over m unfolds to the one over p1."""
+    rng = np.random.default_rng(11)
+    st, g = _state(rng, H0, W0, K)
+    m = oc.SmallCNN(st, K)
+    B = 5
+    x = rng.standard_normal((B, 1, H0, W0))
+    out, c = m.forward_train(x, np.ones((B, g["flat"])), np.ones((B, 128)))
+    r1, bn = c["r1"], c["bn1"]
+    gam, bet = m.p["bn1.weight"], m.p["bn1.bias"]
+    alpha = gam * bn["invstd"]
+    betap = bet - bn["mean"] * alpha
+    W1p = g["W1p"]
+    win = r1[:, :, :, :3 * W1p].reshape(B, 64, g["H1"], W1p, 3)
+    msel = np.where((gam < 0)[None, :, None, None], win.min(-1), win.max(-1))
+    p1 = alpha[None, :, None, None] * msel + betap[None, :, None, None]
+    np.testing.assert_allclose(p1, c["in2"], rtol=1e-12, atol=1e-12)
+    W2, b2 = m.p["conv2.weight"], m.p["conv2.bias"]
+    wf = W2 * alpha[None, :, None, None]
+    bf = b2 + np.einsum("ncij,c->n", W2, betap)
+    np.testing.assert_allclose(oc.conv2x2(msel, wf, bf), oc.conv2x2(c["in2"], W2, b2), rtol=1e-10, atol=1e-10)
+    dz = rng.standard_normal((B, 64, g["H2"], g["W2"]))
+    _, gm, db = oc.conv2x2_backward(msel, W2, dz, need_dx=False)
+    _, gp, _ = oc.conv2x2_backward(c["in2"], W2, dz, need_dx=False)
+    unf = alpha[None, :, None, None] * gm + betap[None, :, None, None] * db[:, None, None, None]
+    np.testing.assert_allclose(unf, gp, rtol=1e-10, atol=1e-10)
