@@ -707,10 +707,16 @@ __global__ void __launch_bounds__(kT) conv1_dx_kernel(const float* __restrict__ 
 // ------------------------------------------------------------------ BN statistics
 // part layout: [(j*C + c) * nblk + blk], j = 0 sum, 1 sumsq
 // nbt (optional): BatchNorm num_batches_tracked of all three layers, incremented once
+// fw != nullptr (BN1 folded into conv2, conv1_stats_fold_kernel): block c also writes conv2's folded
+// weights fwo = fw * alpha_c for input channel c (fw: the [co][tap][ci] repack, 64 output channels)
+// and ft[c][n] = sum_tap fw[n][tap][c] * beta'_c (double) for the folded bias
 __global__ void __launch_bounds__(kT) bn_finalize_kernel(const float* part, int nblk, int C, double count,
                                                          const float* gamma, const float* beta, float* rm, float* rv,
-                                                         float4* coef, int64_t* nbt = nullptr) {
+                                                         float4* coef, int64_t* nbt = nullptr,
+                                                         const float* fw = nullptr, float* fwo = nullptr,
+                                                         double* ft = nullptr) {
   const int c = blockIdx.x;
+  __shared__ float fab[2];
   if (nbt != nullptr && c == 0 && threadIdx.x < 3) nbt[threadIdx.x] += 1;
   double s = 0.0, ss = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) {
@@ -735,11 +741,27 @@ __global__ void __launch_bounds__(kT) bn_finalize_kernel(const float* part, int 
     const float alpha = gamma[c] * invstd;
     const float meanf = (float)mean;
     coef[c] = make_float4(meanf, invstd, alpha, beta[c] - meanf * alpha);
+    fab[0] = alpha;
+    fab[1] = beta[c] - meanf * alpha;
     if (rm) {
       const double mo = (double)kMomentum;
       rm[c] = (float)(mo * mean + (1.0 - mo) * (double)rm[c]);
       rv[c] = (float)(mo * (var * count / (count - 1.0)) + (1.0 - mo) * (double)rv[c]);
     }
+  }
+  if (fw == nullptr) return;
+  __syncthreads();
+  const float al = fab[0], bp = fab[1];
+  for (int q = threadIdx.x; q < 64 * 4; q += kT) {  // q = co * 4 + tap
+    const int64_t e = (int64_t)q * C + c;
+    fwo[e] = fw[e] * al;
+  }
+  if (threadIdx.x < 64) {
+    const int n = threadIdx.x;
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = fma((double)fw[(int64_t)(n * 4 + t) * C + c], (double)bp, acc);
+    ft[(int64_t)c * 64 + n] = acc;
   }
 }
 
@@ -1321,10 +1343,10 @@ struct NTArgs {
   int nblk;
   DropArgs drop;  // EPI_FC1 (dropout2 on relu(fc1)), EPI_DROPGRAD (dropout1 mask)
   int ksplit;     // EPI_PARTIAL: K chunks split over blockIdx.z, raw sums to out[z][M][ldc]
-  // conv_ws_split_kernel, EPI_CONV: the source holds m with src = alpha_ci m + beta'_ci (BN coefficient
-  // float4 (mean, invstd, alpha, beta') per input channel): alpha folded into the weights, the
-  // beta' terms into the bias (conv1_stats_fold_kernel)
-  const float4* fold;
+  // conv_ws_split_kernel, EPI_CONV: the source holds m with src = alpha_ci m + beta'_ci
+  // (conv1_stats_fold_kernel); Bw holds the weights times alpha and fold_t[ci][n] the beta' terms of
+  // the bias (bn_finalize_kernel), summed into it in the prologue
+  const double* fold_t;
   // gemm_nt_kernel, EPI_DROPGRAD (fc1 data gradient): part != nullptr also forms BN3's backward sums
   // sum dy and sum dy * xhat, xhat = (p3d / scale - beta) / gamma over the stored dropout output p3d
   // (dropped elements have dy = 0), one partial pair per block; bias = beta, bn_period = columns per
@@ -1804,36 +1826,29 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3][N * LD];
   __shared__ float red[WPB][N][2];
   __shared__ float bfold[N];
-  static_assert((N * (K / 8)) % (WPB * 64) == 0 && (K / 8) <= 64, "fold: whole lane groups per weight row");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // ---- weights -> three exact bf16 planes, [plane][n][k] with k = tap * CS + channel
   for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
     const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
-    float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
-    float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
-    if (EPI == EPI_CONV && a.fold != nullptr) {  // w * alpha_ci, rounded once; bias b_n + sum_k w beta'_ci
-      const int ci = k8 % CS;
-      const float wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      double bs = 0.0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) bs = fma((double)wv[i], (double)a.fold[ci + i].w, bs);
-      // the K / 8 chunks of row n are K / 8 consecutive lanes (N * K / 8 is a multiple of the block)
-#pragma unroll
-      for (int o = K / 16; o > 0; o >>= 1) bs += __shfl_xor(bs, o, 64);
-      if (idx % (K / 8) == 0) bfold[n] = (float)(bs + (double)a.bias[n]);
-      lo.x *= a.fold[ci].z;
-      lo.y *= a.fold[ci + 1].z;
-      lo.z *= a.fold[ci + 2].z;
-      lo.w *= a.fold[ci + 3].z;
-      hi.x *= a.fold[ci + 4].z;
-      hi.y *= a.fold[ci + 5].z;
-      hi.z *= a.fold[ci + 6].z;
-      hi.w *= a.fold[ci + 7].z;
-    }
+    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
     bf16x8 pl[3];
     split3_x8(lo, hi, pl);
 #pragma unroll
     for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
+  }
+  if (EPI == EPI_CONV && a.fold_t != nullptr) {
+    // folded bias b_n + sum_c ft[c][n] (bn_finalize_kernel), 8 lanes per output channel; a.Bw holds
+    // the folded weights
+    for (int q = tid; q < N * 8; q += WPB * 64) {
+      const int n = q / 8, part = q % 8;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < CS / 8; ++c) acc += a.fold_t[(int64_t)(part * (CS / 8) + c) * N + n];
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) bfold[n] = (float)(acc + (double)a.bias[n]);
+    }
   }
   __syncthreads();
   // ---- this wave's rows [r_lo, r_hi): an even split of M over every wave of the grid
@@ -1852,7 +1867,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   for (int j = 0; j < NJ; ++j) {
     st[j][0] = st[j][1] = 0.0f;
     bias[j] = 0.0f;
-    if constexpr (EPI == EPI_CONV) bias[j] = a.fold != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
+    if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
   }
   // One continuous stream of K steps over all of this wave's tiles (KS steps per TR-row tile):
   // the A loads run PDW steps ahead ACROSS tile boundaries, so the pipeline never drains at a
@@ -3095,6 +3110,8 @@ struct Work {
   float *w2f, *w2d, *w3f, *w3d, *f1t;
   float* part;
   float *partb3, *partb2;  // BN3 / BN2 backward-apply bias partials (read by the side stream's slab reduction)
+  float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
+  double* ft2;             //   and the beta' bias terms [ci][co]
   float* slab;
   float* slab2;   // group sums of slab (hierarchical reduce) / fc1 split-K partials
   float4* coef;   // 3 x 64
@@ -3190,6 +3207,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   w.mask2 = reinterpret_cast<uint8_t*>(take((size_t)B * 128));
   w.partb3 = F(4096LL * 64);  // grid_for caps the apply grids at 4096 blocks
   w.partb2 = F(4096LL * 64);
+  w.w2fold = F(64 * 256);     // BN1 fold: conv2 weights times alpha, bias terms (double)
+  w.ft2 = reinterpret_cast<double*>(take(64 * 64 * sizeof(double)));
   w.bytes = off;
   return w;
 }
@@ -3652,10 +3671,13 @@ int sync_point(const BnSync& y, int point, int C) {
 }
 
 // train-mode BatchNorm statistics -> coefficients (+ running statistics), per rank or synchronised
+// fw / fwo / ft: BN1 fold outputs (bn_finalize_kernel; single rank only: bn1_fold_ok excludes SyncBN)
 int bn_fwd_finalize(const BnSync& y, int point, const float* part, int nblk, int C, double count, const float* gamma,
-                    const float* beta, float* rm, float* rv, float4* coef, int64_t* nbt, hipStream_t s) {
+                    const float* beta, float* rm, float* rv, float4* coef, int64_t* nbt, hipStream_t s,
+                    const float* fw = nullptr, float* fwo = nullptr, double* ft = nullptr) {
+  ABD_CHECK(fw == nullptr || !y.on(), ABD_E_UNSUPPORTED, "BN1 fold with SyncBN");
   if (!y.on()) {
-    bn_finalize_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, gamma, beta, rm, rv, coef, nbt);
+    bn_finalize_kernel<<<C, kT, 0, s>>>(part, nblk, C, count, gamma, beta, rm, rv, coef, nbt, fw, fwo, ft);
     ABD_LAUNCH_CHECK();
     return 0;
   }
@@ -3753,7 +3775,8 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     abd::prof_end(abd::PH_CONV1_STATS, s);
     ABD_LAUNCH_CHECK();
     if (bn_fwd_finalize(sy, 0, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], P.p[P_BN1B], rmu[0],
-                        rvu[0], w.coef, running_upd ? nbt : nullptr, s))
+                        rvu[0], w.coef, running_upd ? nbt : nullptr, s, fold1 ? w.w2f : nullptr,
+                        fold1 ? w.w2fold : nullptr, fold1 ? w.ft2 : nullptr))
       return -1;
   } else {
     bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN1W], P.p[P_BN1B], rm[0], rv[0], 64, w.coef);
@@ -3778,7 +3801,10 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     a.part = (train && !inst) ? w.part : nullptr;
     // p1 holds m under the BN1 fold: only the weight-stationary split kernel applies it (bn1_fold_ok)
     ABD_CHECK(!fold1 || ws, ABD_E_UNSUPPORTED, "BN1 fold needs the weight-stationary conv2 kernel");
-    if (fold1) a.fold = w.coef;
+    if (fold1) {
+      a.Bw = w.w2fold;
+      a.fold_t = w.ft2;
+    }
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
            : ws ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD)
@@ -4292,7 +4318,7 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   Params P = params_of(net, a->params);
   // the weight repacks ride on conv1_stats_kernel's launch (forward(..., prep))
   const PrepArgs prep = prep_args(P, w, g);
-  const bool fold1 = bn1_fold_ok(net, g, B);
+  const bool fold1 = bn1_fold_ok(net, g, B) && !bn_sync_of(a).on();  // the fold rides on the single-rank finalize
   DropArgs d1 = make_drop(a, 1, w.mask1, g.flat), d2 = make_drop(a, 2, w.mask2, 128);
   const BnSync sy = bn_sync_of(a);
   if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep,
