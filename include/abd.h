@@ -231,9 +231,10 @@ size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch);
 /* Byte offset of a named activation buffer inside the workspace (tests / debugging):
  * p1 r2 p2 r3 p3d d2 logp dz dp3 da dz3 dp2 dz2 dp1 coef bcoef mask1 mask2 rowinfo. */
 int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name);
-/* 1 when abd_smallcnn_train_step at this batch folds BN1 into conv2 (f32split, no SyncBN): the workspace's p1
- * then holds m, the pool1-selected relu(conv1) value per window, and p1 = alpha * m + beta' with
- * BN1's coefficients (coef[0][c] = (mean, invstd, alpha, beta')); 0 otherwise. */
+/* 1 when abd_smallcnn_train_step at this batch folds BN1 into conv2 (ABD_PREC_F32_SPLIT; a step
+ * with SyncBN (abd_train_args.bn_sync set) never folds): the workspace's p1 then holds m, the
+ * pool1-selected relu(conv1) value per window, and p1 = alpha * m + beta' with BN1's coefficients
+ * (coef[0][c] = (mean, invstd, alpha, beta')); 0 otherwise. */
 int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch);
 
 /* Device-side counters written by the train/eval launches (int64 / double):
