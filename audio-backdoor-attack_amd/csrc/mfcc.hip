@@ -24,6 +24,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdlib>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -1707,21 +1708,32 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
 #ifdef ABD_MEL_W_LDS
   lds += (size_t)((d.mel2_total + 3) & ~3) * 4;
 #endif
-  // residency from the occupancy API (VGPRs + LDS), cached per LDS size
+  // residency from the occupancy API (VGPRs + LDS), cached per LDS size (host threads may launch
+  // concurrently on different streams: the cache is guarded, the launch itself holds no state)
+  static std::mutex mu;
   static size_t cached_lds = 0;
-  static int cached_blocks = 0, n_cu = 0;
-  if (cached_lds != lds) {
-    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-    int dev = 0, nb = 0;
-    ABD_HIP(hipGetDevice(&dev));
-    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kern), kThreads, lds));
-    cached_blocks = std::max(1, nb);
-    cached_lds = lds;
+  static int cached_blocks = 0, cached_cu = 0;
+  int resident = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (cached_lds != lds) {
+      ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      int dev = 0, nb = 0, ncu = 0;
+      ABD_HIP(hipGetDevice(&dev));
+      ABD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kern), kThreads, lds));
+      cached_blocks = std::max(1, nb);
+      cached_cu = ncu;
+      cached_lds = lds;
+    }
+    resident = cached_cu * cached_blocks;
   }
+  // ABD_STFT_MAX_BLOCKS caps the persistent grid (tests: every block then walks many items, the
+  // loop-carried path -- next-item hand-off, stealing, LDS reuse across items -- at any batch)
+  if (const char* cap = getenv("ABD_STFT_MAX_BLOCKS")) resident = std::max(1, std::min(resident, atoi(cap)));
   const int64_t items = batch * d.chunks;
-  const int grid = (int)std::min<int64_t>(items, (int64_t)n_cu * cached_blocks);
+  const int grid = (int)std::min<int64_t>(items, (int64_t)resident);
   ABD_HIP(hipMemsetAsync(queue, 0, kQueues * kQueueStride * sizeof(unsigned), s));
   kern<<<grid, kThreads, lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue);
   ABD_LAUNCH_CHECK();

@@ -457,7 +457,27 @@ __global__ void __launch_bounds__(kT) conv1_stats_fold_kernel(C1Args a) {
 }
 
 // backward stats: s1 = sum dy, s2 = sum dy * xhat over pool1 argmax positions
-__global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) {
+// The derived BatchNorm backward statistics (bn_bwd_derived_kernel, slab_reduce_derive_kernel, the fc1
+// data-gradient epilogue for BN3) read xhat back from the stored BN output as (p - beta) / gamma: the
+// fp32 rounding of p is amplified by |beta| / |gamma|, and at gamma = 0 p holds no xhat at all
+// (ADVICE r2).  A channel is "tiny" when |gamma| <= 1e-2 |beta| + 1e-5 (amplification <= 100x:
+// <= ~6e-6 relative); the guarded kernels below then recompute the whole layer's statistics from the
+// activations (the passes the derivation replaced) and exit at once otherwise.  Wave-uniform, C <= 64.
+__device__ __forceinline__ bool bn_any_tiny(const float* __restrict__ gamma, const float* __restrict__ beta, int C) {
+  const int lane = threadIdx.x & 63;
+  bool t = false;
+  if (lane < C) t = fabsf(gamma[lane]) <= 1e-2f * fabsf(beta[lane]) + 1e-5f;
+  return __ballot(t) != 0ull;
+}
+
+__device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a);
+__global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) { conv1_bwd_stats_body(a); }
+// guarded fallback: BN1's statistics from the activations when a gamma is tiny (bn_any_tiny)
+__global__ void __launch_bounds__(kT) conv1_bwd_stats_guard_kernel(C1Args a, const float* gamma, const float* beta) {
+  if (!bn_any_tiny(gamma, beta, 64)) return;
+  conv1_bwd_stats_body(a);
+}
+__device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
@@ -878,7 +898,10 @@ __global__ void bn_eval_bcoef_kernel(const float4* coef, int C, BCoef* bcoef) {
 // backward finalize: s1 = sum dy (-> dbeta), s2 = sum dy*xhat (-> dgamma); coefficients for dx
 __global__ void __launch_bounds__(kT) bn_bwd_finalize_kernel(const float* part, int nblk, int C, double count,
                                                              const float* gamma, const float4* coef, float* dgamma,
-                                                             float* dbeta, BCoef* bcoef) {
+                                                             float* dbeta, BCoef* bcoef,
+                                                             const float* guard_beta = nullptr) {
+  // guard_beta != nullptr: the guarded fallback's finalize (runs only when a gamma is tiny)
+  if (guard_beta != nullptr && !bn_any_tiny(gamma, guard_beta, C)) return;
   const int c = blockIdx.x;
   double s1 = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < nblk; i += kT) {
@@ -1009,10 +1032,11 @@ __device__ __forceinline__ float unfold_wgrad(float gm, const float4* fold, cons
   return fold ? (float)fma((double)fold[ci].z, (double)gm, (double)fold[ci].w * (double)db[n]) : gm;
 }
 
-// block-reduce this thread's (s1, s2) share of channel c and write its BN backward outputs
+// block-reduce this thread's (s1, s2) share of channel c and write its BN backward outputs;
+// folded: s2 is sum W (G_m - mean db), scaled by invstd instead of divided by gamma
 __device__ __forceinline__ void bn_bwd_derived_finish(int c, double s1, double s2, int Cin, const float* gamma,
                                                       const float4* coef, double count, float* dgamma, float* dbeta,
-                                                      BCoef* bcoef, double* sums) {
+                                                      BCoef* bcoef, double* sums, bool folded = false) {
   __shared__ double red[2][kT / kWave];
   s1 = abd::wave_sum_d(s1);
   s2 = abd::wave_sum_d(s2);
@@ -1023,7 +1047,8 @@ __device__ __forceinline__ void bn_bwd_derived_finish(int c, double s1, double s
   __syncthreads();
   if (threadIdx.x == 0) {
     s1 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    s2 = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (double)gamma[c];
+    s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    s2 = folded ? s2 * (double)coef[c].y : s2 / (double)gamma[c];
     dgamma[c] = (float)s2;
     dbeta[c] = (float)s1;
     if (sums) {
@@ -1075,18 +1100,23 @@ __global__ void __launch_bounds__(kT) slab_reduce_derive_kernel(const float* sla
                                                                 int Cin, float* out, DeriveArgs d) {
   const int c = blockIdx.x;
   const int64_t total = (int64_t)Cout * Ktot;
-  const double b = (double)d.beta[c];
+  // folded source m (BN1 fold): xhat of the pool-selected element is (m - mean) invstd, so
+  //   sum dy xhat = invstd sum_{n,t} W (G_m - mean db)  -- no division by gamma
+  // otherwise xhat = (p - beta) / gamma from the stored BN output p
+  const double b = d.fold ? (double)d.coef[c].x : (double)d.beta[c];
   double s1 = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < Cout * 4; i += kT) {
     const int n = i >> 2, t = i & 3;
-    const float gv = unfold_wgrad(ordered_sum(slab + (int64_t)n * Ktot + t * Cin + c, total, nslab), d.fold, d.db, n, c);
+    const float gm = ordered_sum(slab + (int64_t)n * Ktot + t * Cin + c, total, nslab);
+    const float gv = unfold_wgrad(gm, d.fold, d.db, n, c);
     const int64_t o = ((int64_t)n * Cin + c) * 4 + t;
     out[o] = gv;
     const double w = (double)d.W[o], dbn = (double)d.db[n];
     s1 = fma(w, dbn, s1);
-    s2 = fma(w, fma(-b, dbn, (double)gv), s2);
+    s2 = fma(w, fma(-b, dbn, (double)(d.fold ? gm : gv)), s2);
   }
-  bn_bwd_derived_finish(c, s1, s2, Cin, d.gamma, d.coef, d.count, d.dgamma, d.dbeta, d.bcoef, nullptr);
+  bn_bwd_derived_finish(c, s1, s2, Cin, d.gamma, d.coef, d.count, d.dgamma, d.dbeta, d.bcoef, nullptr,
+                        d.fold != nullptr);
 }
 
 
@@ -1250,7 +1280,15 @@ __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
 }
 
 // BN backward sums over pooled outputs: sum dy, sum dy * xhat(r at the argmax)
-__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) {
+__device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a);
+__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) { bn_pool_bwd_stats_body(a); }
+// guarded fallback: BN2 / BN3 statistics from the activations when a gamma is tiny (bn_any_tiny)
+__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_guard_kernel(PoolArgs a, const float* gamma,
+                                                                     const float* beta) {
+  if (!bn_any_tiny(gamma, beta, a.C)) return;
+  bn_pool_bwd_stats_body(a);
+}
+__device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a) {
   const int CG = a.C / 4;
   const int total = a.B * a.Ho * a.Wo * CG;
   const int c0 = (threadIdx.x % CG) * 4;  // fixed per thread: grid stride is a multiple of CG
@@ -2898,7 +2936,10 @@ __global__ void __launch_bounds__(kT) fc2_loss_kernel(LossArgs a) {
 }
 
 // one block: deterministic batch reduction -> metrics (loss mean as double bits, counts)
-__device__ __forceinline__ void metrics_body(const float* rowinfo, int B, int64_t* metrics) {
+// lw: the batch-mean loss is weighted by lw before it is accumulated -- data parallelism passes
+// B_local / B_global, so the per-rank words SUM over ranks to the global batch mean even when
+// the last batch of an epoch splits unevenly (parallel_dp.reduce_metrics)
+__device__ __forceinline__ void metrics_body(const float* rowinfo, int B, int64_t* metrics, double lw = 1.0) {
   double s = 0.0;
   long long c = 0, p = 0, h = 0;
   for (int i = threadIdx.x; i < B; i += kT) {
@@ -2923,7 +2964,7 @@ __device__ __forceinline__ void metrics_body(const float* rowinfo, int B, int64_
   }
   if (threadIdx.x == 0) {
     double acc = __longlong_as_double(metrics[0]);
-    acc += rs[0] / B;
+    acc += rs[0] * lw / B;
     metrics[0] = __double_as_longlong(acc);
     metrics[1] += B;
     metrics[2] += rc[0][0];
@@ -2985,10 +3026,10 @@ __global__ void __launch_bounds__(128) fc2_wgrad_kernel(const float* dz, const f
 // metrics != nullptr: the last block reduces the loss kernel's per-row flags into the counters
 __global__ void __launch_bounds__(kT) fc2_grads_kernel(const float* dz, const float* d2, const float* w2, int B, int K,
                                                        int rows, int nsplit, float* part, float scale2, float* da,
-                                                       int nw, const float* rowinfo, int64_t* metrics) {
+                                                       int nw, const float* rowinfo, int64_t* metrics, double lw) {
   const int nb = (int)gridDim.x - (metrics ? 1 : 0);
   if (metrics && (int)blockIdx.x == nb) {
-    metrics_body(rowinfo, B, metrics);
+    metrics_body(rowinfo, B, metrics, lw);
     return;
   }
   if ((int)blockIdx.x < nw) {
@@ -3966,15 +4007,32 @@ int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
   return 0;
 }
 
+// Guarded fallback of the derived BN2 / BN3 backward statistics (bn_any_tiny): the activation pass
+// and its finalize over at most kGuardBlocks blocks, both exiting at once unless a gamma is tiny;
+// they overwrite dgamma / dbeta / bcoef written by the derivation.  w.part is free at this point.
+constexpr int kGuardBlocks = 256;
+int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, double count, const float4* coef,
+                 float* dgamma, float* dbeta, BCoef* bcoef, hipStream_t s) {
+  PoolArgs pa = pa_in;
+  pa.nblk = std::min(grid_for((int64_t)pa.B * pa.Ho * pa.Wo * pa.C / 4), kGuardBlocks);
+  bn_pool_bwd_stats_guard_kernel<<<pa.nblk, kT, 0, s>>>(pa, gamma, beta);
+  ABD_LAUNCH_CHECK();
+  bn_bwd_finalize_kernel<<<pa.C, kT, 0, s>>>(pa.part, pa.nblk, pa.C, count, gamma, coef, dgamma, dbeta, bcoef, beta);
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
+
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
-             int64_t* metrics = nullptr, bool fold1 = false) {
+             int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0) {
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   const hipStream_t sw = wgrad_stream(net, s);
-  const bool derive = bn_bwd_derived_on();
+  // SyncBN steps take the activation passes: the derived sums' small-gamma fallback (below) is decided
+  // on the device, where the host-issued all-reduce of a second set of sums cannot follow it
+  const bool derive = bn_bwd_derived_on() && !sy.on();
   int bn3_parts = 0;  // > 0: BN3 backward partials from the fc1 data-gradient epilogue
-  // derived in the weight gradients' last reduction; SyncBN all-reduces the sums first (separate kernel)
-  const bool derive_fused = derive && !sy.on();
+  // derived in the weight gradients' last reduction
+  const bool derive_fused = derive;
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -3986,7 +4044,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     // two launches instead of four: [fc2 weight-grad partials | da] then [their reduction | fc1 bias]
     const int nw = (g.K * kFc2Split + 1) / 2;
     fc2_grads_kernel<<<(unsigned)(nw + grid_for(B * 128) + (metrics ? 1 : 0)), kT, 0, s>>>(
-        w.dz, w.d2, P.p[P_F2W], (int)B, g.K, rows, kFc2Split, w.slab2, s2, w.da, nw, w.rowinfo, metrics);
+        w.dz, w.d2, P.p[P_F2W], (int)B, g.K, rows, kFc2Split, w.slab2, s2, w.da, nw, w.rowinfo, metrics, loss_w);
     fc2_reduce_colsum_kernel<<<(unsigned)(128 + (g.K * 129 + kT - 1) / kT), kT, 0, s>>>(
         w.slab2, kFc2Split, g.K, G[P_F2W], G[P_F2B], w.da, (int)B, 128, G[P_F1B]);
   }
@@ -4038,7 +4096,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     // BN3's backward sums in this epilogue (32-column tiles within one channel)
     static const bool bn3f = env_int("ABD_BN3_FUSED", 1) != 0;
     const int per3 = g.flat / 32;  // columns per BN3 channel (flatten order c, h, w)
-    if (bn3f && drop1.enabled && per3 % 32 == 0 && env_int("ABD_FC1D_NB", 32) == 32) {
+    if (bn3f && !sy.on() && drop1.enabled && per3 % 32 == 0 && env_int("ABD_FC1D_NB", 32) == 32) {
       a.part = w.part;
       a.bias = P.p[P_BN3B];
       a.bn_gamma = P.p[P_BN3W];
@@ -4074,6 +4132,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     }
     if (bn_bwd_finalize(sy, 3, w.part, pa.nblk, 32, (double)B * g.H3 * g.W3, P.p[P_BN3W], w.coef + 128, G[P_BN3W],
                         G[P_BN3B], w.bcoef + 128, s))
+      return -1;
+    if (bn3_parts > 0 && bn_bwd_guard(pa, P.p[P_BN3W], P.p[P_BN3B], (double)B * g.H3 * g.W3, w.coef + 128, G[P_BN3W],
+                                      G[P_BN3B], w.bcoef + 128, s))
       return -1;
     pa.bcoef = w.bcoef + 128;
     pa.dz = w.dz3;
@@ -4125,6 +4186,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
           (!derive_fused &&
            bn_bwd_derive(sy, 4, P.p[P_C3W], G[P_C3W], G[P_C3B], 32, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W],
                          P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s)))
+        return -1;
+      if (bn_bwd_guard(pa, P.p[P_BN2W], P.p[P_BN2B], (double)B * g.H2 * g.W2, w.coef + 64, G[P_BN2W], G[P_BN2B],
+                       w.bcoef + 64, s))
         return -1;
     } else {
       bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
@@ -4194,6 +4258,15 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
            bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
                          P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s)))
         return -1;
+      if (!fold1) {  // the folded derivation has no division by gamma; otherwise guard it
+        C1Args c1g = c1;
+        c1g.nblk = (int)std::min<int64_t>(c1.nblk, kGuardBlocks);
+        conv1_bwd_stats_guard_kernel<<<c1g.nblk, kT, 0, s>>>(c1g, P.p[P_BN1W], P.p[P_BN1B]);
+        ABD_LAUNCH_CHECK();
+        bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1g.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef,
+                                                 G[P_BN1W], G[P_BN1B], w.bcoef, P.p[P_BN1B]);
+        ABD_LAUNCH_CHECK();
+      }
     } else {
       conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
       ABD_LAUNCH_CHECK();
@@ -4284,7 +4357,7 @@ size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch) {
 }
 
 int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch) {
-  return (net && batch >= 2 && bn1_fold_ok(net, net->g, batch)) ? 1 : 0;
+  return (net && batch >= 1 && bn1_fold_ok(net, net->g, batch)) ? 1 : 0;
 }
 
 int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name) {
@@ -4307,7 +4380,9 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
                             abd_stream_t stream) {
   ABD_CHECK(net && a && a->x && a->labels && a->params && a->grads && a->running, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
-  ABD_CHECK(B >= 2, ABD_E_INVALID, "train step needs batch >= 2 (BatchNorm), got %lld", (long long)B);
+  // BatchNorm2d normalises over N x H x W, so one row is a valid train-mode batch (the loader's
+  // 1-row tail, drop_last=False)
+  ABD_CHECK(B >= 1, ABD_E_INVALID, "train step needs batch >= 1, got %lld", (long long)B);
   ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",
@@ -4327,7 +4402,8 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
   // the metrics reduction rides on backward()'s fc2 gradient launch
   if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1)) return -1;
+  const double loss_w = a->grad_scale > 0.0f ? (double)a->grad_scale : 1.0;
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w)) return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
@@ -4370,7 +4446,7 @@ int abd_smallcnn_backward(abd_cnn* net, const abd_train_args* a, const float* dl
                           size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(net && a && a->x && a->params && a->grads && dlogprobs, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
-  ABD_CHECK(B >= 2, ABD_E_INVALID, "backward needs batch >= 2 (BatchNorm), got %lld", (long long)B);
+  ABD_CHECK(B >= 1, ABD_E_INVALID, "backward needs batch >= 1, got %lld", (long long)B);
   ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small");

@@ -137,7 +137,7 @@ class SelectionModel:
             need = L.lib().abd_smallcnn_forward_per_utterance_workspace_bytes(eng.h, e - s)
             if self._ws is None or self._ws.numel() < need:
                 self._ws = torch.empty(need, dtype=torch.uint8, device=x.device)
-            sd = dropout_seed(x.device) if seed is None else seed
+            sd = dropout_seed(x.device, m) if seed is None else seed
             rc = L.lib().abd_smallcnn_forward_per_utterance(
                 eng.h, x[s:e].data_ptr(), e - s, eng.params.data_ptr(), sd, m._step,
                 mask1[s:e].data_ptr() if mask1 is not None else None,

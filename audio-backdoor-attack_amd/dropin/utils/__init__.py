@@ -14,10 +14,20 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _other_portions():
+    """The reference checkout's ``utils`` directory.  ``abd_amd.run`` names it (the attack
+    script's directory, ABD_REFERENCE_ROOT); otherwise only a ``utils`` directory whose parent
+    looks like the reference checkout (it holds ``prepare_dataset.py``) is taken, so an unrelated
+    ``utils`` package on sys.path (site-packages, the CWD) is never executed in its place."""
+    root = os.environ.get("ABD_REFERENCE_ROOT")
+    if root:
+        d = os.path.join(os.path.abspath(root), "utils")
+        return [d] if os.path.isdir(d) and os.path.realpath(d) != os.path.realpath(_HERE) else []
     out = []
     for entry in sys.path:
-        d = os.path.join(os.path.abspath(entry or os.getcwd()), "utils")
-        if os.path.isdir(d) and os.path.realpath(d) != os.path.realpath(_HERE) and d not in out:
+        base = os.path.abspath(entry or os.getcwd())
+        d = os.path.join(base, "utils")
+        if (os.path.isdir(d) and os.path.isfile(os.path.join(base, "prepare_dataset.py"))
+                and os.path.realpath(d) != os.path.realpath(_HERE) and d not in out):
             out.append(d)
     return out
 

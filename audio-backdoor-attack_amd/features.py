@@ -57,7 +57,6 @@ class MfccPlan:
         L.check(rc, "abd_mfcc_plan_create")
         self._h = h
         self.n_frames = lib.abd_mfcc_plan_frames(h)
-        self._ws = None
 
     def describe(self):
         m, blue, npass = C.c_int(), C.c_int(), C.c_int()
@@ -66,11 +65,15 @@ class MfccPlan:
         return {"fft_size": m.value, "bluestein": bool(blue.value), "radices": list(rad[:npass.value]),
                 "n_frames": self.n_frames}
 
+    def workspace_bytes(self, batch: int) -> int:
+        return int(L.lib().abd_mfcc_workspace_bytes(self._h, int(batch)))
+
     def workspace(self, batch: int) -> torch.Tensor:
-        need = L.lib().abd_mfcc_workspace_bytes(self._h, int(batch))
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        return self._ws
+        """A fresh workspace for one launch of ``batch`` rows, from the caching allocator on the
+        current stream.  The plan itself holds no per-call device state (ops are
+        re-entrant): two launches on two streams get two workspaces, so neither the STFT's item
+        queues (zeroed per launch) nor its dB intermediate can be shared between them."""
+        return torch.empty(max(self.workspace_bytes(batch), 1), dtype=torch.uint8, device=self.device)
 
     def __del__(self):
         try:
@@ -133,8 +136,13 @@ class Injection:
 
 def mfcc_batch(waves: torch.Tensor, cfg: MfccConfig, rows: torch.Tensor | None = None,
                inject: Injection | None = None, out: torch.Tensor | None = None,
-               batch: int | None = None) -> torch.Tensor:
-    """waves (N, >=L) fp32 on device -> (B, 1, T, n_mfcc); rows (int32, B) gathers the batch."""
+               batch: int | None = None, workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """waves (N, >=L) fp32 on device -> (B, 1, T, n_mfcc); rows (int32, B) gathers the batch.
+
+    ``workspace`` (uint8, >= ``plan.workspace_bytes(B)``) is caller-owned scratch; the caller
+    orders its reuse (the resident trainer keeps one per stream).  Without it each call takes a
+    fresh block from the caching allocator on the current stream, so concurrent calls on
+    different streams never share scratch."""
     L.require_device(waves, "waves")
     assert waves.dtype == torch.float32 and waves.dim() == 2 and waves.shape[1] >= cfg.length
     plan = get_plan(cfg, waves.device)
@@ -145,7 +153,11 @@ def mfcc_batch(waves: torch.Tensor, cfg: MfccConfig, rows: torch.Tensor | None =
         B = waves.shape[0] if batch is None else batch
     if out is None:
         out = torch.empty((B, 1, plan.n_frames, cfg.n_mfcc), dtype=torch.float32, device=waves.device)
-    ws = plan.workspace(B)
+    if workspace is None:
+        ws = plan.workspace(B)
+    else:
+        assert workspace.dtype == torch.uint8 and workspace.is_cuda and workspace.numel() >= plan.workspace_bytes(B)
+        ws = workspace
     inj = inject.to_c() if inject is not None else None
     rc = L.lib().abd_mfcc_f32(plan._h, waves.data_ptr(), waves.stride(0),
                              rows.data_ptr() if rows is not None else None, B,

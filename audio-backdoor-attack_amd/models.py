@@ -12,6 +12,7 @@ running statistics are packed the same way.  The C ABI then sees plain pointers.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 
 import torch
 import torch.nn as nn
@@ -87,15 +88,24 @@ class _Engine:
             pass
 
 
-def dropout_seed(device) -> int:
+_MODEL_NONCE = itertools.count()
+
+
+def dropout_seed(device, model=None) -> int:
     """Seed of the device dropout hash: the device's default torch generator seed (set by
-    torch.manual_seed / fix_random(), utils/random_tools.py:5-18).  Nothing is drawn from the
-    global CPU generator, as on the reference's CUDA path where nn.Dropout consumes the device
-    generator and the CPU stream only feeds the DataLoader shuffles -- so the batch order of
-    every epoch matches the reference's under the same seed."""
+    torch.manual_seed / fix_random(), utils/random_tools.py:5-18), mixed with the model's
+    creation nonce.  Nothing is drawn from the global CPU generator, as on the reference's CUDA
+    path where nn.Dropout consumes the device generator and the CPU stream only feeds the
+    DataLoader shuffles -- so the batch order of every epoch matches the reference's under the
+    same seed.  The nonce (0 for the process's first smallcnn, which keeps the plain seed) gives
+    models built one after another -- flowmur.pretrain_model's surrogates, a re-created model --
+    their own mask streams, as the reference's advancing device generator does; data-parallel
+    ranks build their models in the same order, so they agree on it."""
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    return int(torch.cuda.default_generators[idx].initial_seed()) & ((1 << 63) - 1)
+    base = int(torch.cuda.default_generators[idx].initial_seed())
+    nonce = int(getattr(model, "_dropout_nonce", 0) or 0)
+    return (base + nonce * 0x9E3779B97F4A7C15) & ((1 << 63) - 1)
 
 
 DROPOUT_SOURCES = ("device", "torch_cpu")
@@ -133,6 +143,7 @@ class smallcnn(nn.Module):
         self.softmax = nn.Softmax(dim=1)
         self._engine = None
         self._step = 0
+        self._dropout_nonce = next(_MODEL_NONCE)
         self.gemm_precision = "f32"   # "bf16": conv GEMMs on bf16 MFMA (set_gemm_precision)
         self.dropout_source = "device"  # "torch_cpu": the reference CPU path's exact masks
 
@@ -151,6 +162,14 @@ class smallcnn(nn.Module):
         if getattr(self, "dropout_source", "device") != "torch_cpu":
             return None
         return torch_cpu_masks(batch, self.fc1.in_features, device)
+
+    def __setstate__(self, state):
+        # also the target of reference-format checkpoints (training.ReferencePickle), whose state is
+        # a plain reference smallcnn's __dict__: fill in what this class adds
+        super().__setstate__(state)
+        for k, v in (("_engine", None), ("_step", 0), ("gemm_precision", "f32"), ("dropout_source", "device")):
+            if k not in self.__dict__:
+                self.__dict__[k] = v
 
     def __getstate__(self):
         # the libabd handle is process-local; parameters pickle as ordinary tensors
@@ -249,7 +268,7 @@ class smallcnn(nn.Module):
         ws = eng.workspace(B)
         a = self._args(eng, x, B)
         a.logprobs_out = out.data_ptr()
-        a.seed = dropout_seed(x.device) if seed is None else seed
+        a.seed = dropout_seed(x.device, self) if seed is None else seed
         a.counter = self._step
         self._step += 1
         if mask1 is None:

@@ -5,8 +5,16 @@ takes its contiguous slice of each global batch; the only exchange is ONE sum
 all-reduce of the flat fp32 gradient buffer per step (1.68 MB at 101x40),
 with the loss gradient pre-normalised by the GLOBAL batch inside the loss kernel
 (grad_scale = B_local / B_global), so the summed gradient is the global-batch mean.
+
+The loader's short last batch (DataLoader(shuffle=True), drop_last=False: badnets.py:105-108,
+daba.py:152-154) is split as evenly as it goes (``shard_range``): ranks get floor/ceil shares,
+each weights its gradient and loss by its own count over the global one (§8e "weight gradients
+by the local count before the sum"), and a rank whose share is empty (tail < world) still takes
+part in every collective of the step with zero contributions (``SyncBatchNorm.idle``).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -16,6 +24,16 @@ def shard_slice(pos: int, local_batch: int, rank: int, world: int):
     """[start, stop) of this rank's rows in the global batch that begins at epoch offset ``pos``."""
     s = pos + rank * local_batch
     return s, s + local_batch
+
+
+def shard_range(pos: int, global_rows: int, rank: int, world: int):
+    """[start, stop) of this rank's contiguous share of a global batch of ``global_rows`` rows
+    starting at epoch offset ``pos``: floor(n / world) rows each, the first n % world ranks one
+    more.  A full batch (n = B * world) gives every rank B rows (== shard_slice); a short tail
+    may give a rank none (start == stop)."""
+    q, r = divmod(int(global_rows), int(world))
+    s = pos + rank * q + min(rank, r)
+    return s, s + q + (1 if rank < r else 0)
 
 
 def grad_scale(local_batch: int, global_batch: int) -> float:
@@ -106,6 +124,9 @@ class SyncBatchNorm:
                 return 0
             except Exception as e:  # surfaced as an AbdError by the launch's return code
                 self.error = e
+                # the other ranks are parked in this BN point's all-reduce: tear the group down so
+                # their collectives fail too instead of waiting forever
+                abort_group(self.group)
                 return 1
 
         self._cb = L.BN_SYNC_FN(_sync)   # keep the ctypes thunk alive as long as this object
@@ -117,16 +138,50 @@ class SyncBatchNorm:
         args.bn_sync = self._cb_ptr
         args.bn_sync_ctx = None
 
+    # (C, point) of the 6 synchronised reductions of a train step, in libabd's call order:
+    # forward bn1, bn2, bn3, then backward bn3, bn2, bn1 (smallcnn.hip sync_point)
+    POINTS = ((64, 0), (64, 1), (32, 2), (32, 3), (64, 4), (64, 5))
+
+    def idle(self):
+        """The 6 reductions of a step this rank has no rows for (the tail batch split over more
+        ranks than it has rows): zero sums and zero counts, so the others' statistics are those
+        of the rows that exist.  This rank's running statistics are not updated; they are
+        re-broadcast from rank 0 (which always has rows) before evaluation."""
+        from . import _lib as L
+        for C, point in self.POINTS:
+            off = point * L.BN_SYNC_STRIDE
+            v = self.buf[off:off + 2 * C + 1]
+            v.zero_()
+            dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
+            self.calls += 1
+
+
+def abort_group(group=None):
+    """Fail every rank fast after a local error inside a collective sequence: abort
+    the process group (NCCL/RCCL communicators are torn down, peers' pending collectives error
+    out); if this torch has no abort, destroy it.  ABD_DP_NO_ABORT=1 keeps the group (tests)."""
+    if os.environ.get("ABD_DP_NO_ABORT") == "1":
+        return
+    try:
+        from torch.distributed.distributed_c10d import _abort_process_group
+        _abort_process_group(group)
+    except Exception:
+        try:
+            dist.destroy_process_group(group)
+        except Exception:
+            pass
+
 
 def reduce_metrics(m: torch.Tensor, group=None) -> torch.Tensor:
-    """Combine libabd metric words across ranks: counts summed, batch-mean loss averaged.
+    """Combine libabd metric words across ranks: counts summed, batch-mean losses summed.
 
-    Word 0 holds a float64 (sum of per-batch mean losses); words 1-5 are int64 counts."""
+    Word 0 holds a float64 sum of per-batch mean losses, each already weighted by this rank's
+    B_local / B_global (abd_train_args.grad_scale), so the sum over ranks is the global batch
+    mean also for an uneven last batch; words 1-5 are int64 counts."""
     out = m.clone()
     loss = out[0:1].view(torch.float64).clone()
     dist.all_reduce(loss, group=group)
     world = dist.get_world_size(group)
-    loss /= world
     cnt = out[1:6].clone()
     dist.all_reduce(cnt, group=group)
     out[1:5] = cnt[0:4]

@@ -13,10 +13,13 @@ with no host round trip.  The MFCC of a clip is deterministic, so training sees
 exactly the features the reference caches.
 
 Data parallelism (one process per GPU, torch.distributed over RCCL): every rank
-draws the same epoch permutation and takes its contiguous slice of each global
+draws the same epoch permutation and takes its contiguous share of each global
 batch; gradients (one flat fp32 buffer) are summed with one all-reduce per step and
-normalised by the global batch inside the loss kernel.  BatchNorm statistics are
-per rank (no SyncBN), as in standard DDP.
+normalised by the global batch inside the loss kernel.  The epoch's short last batch
+is kept (the reference's loaders use drop_last=False) and split unevenly, each rank
+weighting by its own row count (parallel_dp.shard_range).  BatchNorm statistics are per
+rank by default, as in standard DDP; ``sync_bn=True`` reduces them over the global
+batch (parallel_dp.SyncBatchNorm).
 """
 from __future__ import annotations
 
@@ -216,6 +219,8 @@ class ResidentTrainer:
         self.plan = F.get_plan(self.mcfg, self.dev)
         self.T = self.plan.n_frames
         self.x = torch.empty((self.B, 1, self.T, cfg.n_mfcc), dtype=torch.float32, device=self.dev)
+        # the feature stage's scratch, owned by this trainer and used on its one stream only
+        self.feat_ws = self.plan.workspace(self.B)
         self.metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=self.dev)
         model.train()
         if gemm_precision is not None:
@@ -244,13 +249,14 @@ class ResidentTrainer:
         self._pos = 0
 
     def _batch_rows(self, pos):
-        """Rows of the global batch starting at pos: a full B * world, or (one rank) the loader's
-        short last batch (drop_last=False); None when the epoch is spent."""
+        """Rows of the global batch starting at pos: a full B * world, or the loader's short last
+        batch (drop_last=False, any size >= 1: BatchNorm2d counts N x H x W per channel); None
+        when the epoch is spent."""
         G = self.B * self.world
         left = self.N - pos
         if left >= G:
             return G
-        if self.world == 1 and left >= 2:   # BatchNorm needs two rows; a 1-row tail is dropped
+        if left >= 1:
             return left
         return None
 
@@ -266,9 +272,9 @@ class ResidentTrainer:
         if self._epoch is None or self._batch_rows(self._pos) is None:
             self.new_epoch()
         g = self._batch_rows(self._pos)
-        b = g // self.world
         rows, lab, ind, pois, pos = self._epoch
-        s, e = DP.shard_slice(self._pos, b, self.rank, self.world)
+        s, e = DP.shard_range(self._pos, g, self.rank, self.world)
+        self._cur = (g, s - self._pos)   # (global rows, global row of this rank's first row)
         self._pos += g
         return rows[s:e], lab[s:e], ind[s:e], pois[s:e], pos[s:e] if pos is not None else None
 
@@ -276,28 +282,41 @@ class ResidentTrainer:
         rows, _, _, pois, pos = batch
         inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois, position=pos,
                           snr_db=self.cfg.snr_db, patch=self.cfg.patch)
-        F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out)
+        F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out, workspace=self.feat_ws)
 
     def step(self):
-        """One global batch: this rank's slice through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
+        """One global batch: this rank's share through inject -> MFCC -> train step [-> all-reduce] -> Adam."""
         batch = self._take_batch()
         b = batch[0].numel()
         x = self.x if b == self.B else self.x[:b]
-        self._features(batch, x)
+        if b > 0:
+            self._features(batch, x)
         self._train(batch, x)
 
     def _train(self, batch, x):
         _, lab, ind, _, _ = batch
+        b = int(lab.numel())
         if self.world == 1:
             T.train_step(self.model, x, lab, ind, self.adam, self.metrics)
-        else:
+            return
+        g, row0 = self._cur
+        if b > 0:
             T.train_step(self.model, x, lab, ind, self.adam, self.metrics, do_update=False,
-                         grad_scale=DP.grad_scale(self.B, self.B * self.world),
-                         fc_grads_event=self.reducer.event_ptr(), row_offset=self.rank * self.B,
-                         bn_sync=self.bn_sync)
-            self.reducer.launch_fc()   # fc grads all-reduce overlaps the conv backward
-            self.reducer.finish()      # conv head all-reduce, join
-            T.apply_adam(self.model, self.adam, self.dev)
+                         grad_scale=DP.grad_scale(b, g), fc_grads_event=self.reducer.event_ptr(),
+                         row_offset=row0, bn_sync=self.bn_sync)
+        else:
+            # the tail batch has fewer rows than there are ranks: nothing to compute here, but this
+            # rank joins every collective of the step with zero contributions
+            eng = self.model._engine
+            eng.grads.zero_()
+            self.model._step += 1      # the dropout stream stays in step with the other ranks
+            if self.bn_sync is not None:
+                self.bn_sync.idle()
+            self.reducer.event.record()
+            self.metrics[5] += 1       # one more global batch seen (reduce_metrics divides by world)
+        self.reducer.launch_fc()   # fc grads all-reduce overlaps the conv backward
+        self.reducer.finish()      # conv head all-reduce, join
+        T.apply_adam(self.model, self.adam, self.dev)
 
     def run_epoch(self):
         self.new_epoch()

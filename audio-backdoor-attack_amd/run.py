@@ -24,6 +24,7 @@ def setup_path(script: str) -> None:
     script_dir = os.path.dirname(os.path.abspath(script))
     rest = [p for p in sys.path if os.path.abspath(p or os.getcwd()) not in (DROPIN, script_dir)]
     sys.path[:] = [DROPIN, script_dir] + rest + ([ROOT] if ROOT not in rest else [])
+    os.environ["ABD_REFERENCE_ROOT"] = script_dir   # the only utils/ the drop-in falls through to
     for name in [m for m in sys.modules if m in ("utils", "prepare_dataset") or m.startswith("utils.")]:
         del sys.modules[name]   # a stale reference import must not shadow the drop-in
 

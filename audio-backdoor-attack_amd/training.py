@@ -10,7 +10,10 @@ element, training_tools.py:71-79).
 """
 from __future__ import annotations
 
+import copy
+import copyreg
 import ctypes as C
+import importlib
 
 import numpy as np
 import torch
@@ -91,7 +94,7 @@ def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None,
             adam.step += 1
             a.adam_step = adam.step
             a.do_update = 1
-    a.seed = dropout_seed(x.device) if seed is None else seed
+    a.seed = dropout_seed(x.device, model) if seed is None else seed
     a.counter = model._step
     model._step += 1
     a.row_offset = int(row_offset)
@@ -125,7 +128,7 @@ def op_train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding, met
     adam.step += 1
     torch.ops.abd.smallcnn_train_step(
         x, labels, indicators, eng.params, eng.grads, eng.exp_avg, eng.exp_avg_sq, eng.running, eng.nbt, metrics,
-        eng.K, adam.step, adam.lr, adam.betas[0], adam.betas[1], adam.eps, dropout_seed(x.device), model._step,
+        eng.K, adam.step, adam.lr, adam.betas[0], adam.betas[1], adam.eps, dropout_seed(x.device, model), model._step,
         hm[0] if hm is not None else None, hm[1] if hm is not None else None, model.gemm_precision)
     model._step += 1
 
@@ -252,6 +255,67 @@ def clean_test(model, device, clean_test_loader, criterion):
     return cl / n, 100 * cc / ct
 
 
+# ------------------------------------------------------------------ reference-format checkpoints
+class _ModuleRef:
+    """Unpickles as ``importlib.import_module(name)`` in the LOADING process."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __reduce__(self):
+        return (importlib.import_module, (self.name,))
+
+
+class _ClassRef:
+    """Unpickles as ``getattr(import_module(module), name)``: the consumer's own class."""
+
+    def __init__(self, module, name):
+        self.module, self.name = module, name
+
+    def __reduce__(self):
+        return (getattr, (_ModuleRef(self.module), self.name))
+
+
+def reference_module_state(model: smallcnn) -> dict:
+    """``__dict__`` of the reference's ``utils.models.smallcnn`` (utils/models.py:17-40) holding this
+    model's parameters and BN buffers: plain nn.Module bookkeeping and the same children in the same
+    order (Conv2d / BatchNorm2d / MaxPool2d / Dropout / Flatten / Linear / Softmax()), each with its
+    own contiguous tensors on the model's device (no view of the flat libabd buffers, no engine)."""
+    ref = nn.Module()
+    for name, child in model.named_children():
+        if name == "softmax":
+            c = nn.Softmax()     # utils/models.py:40 builds it without dim
+        else:
+            c = copy.deepcopy(child)
+            for prm in c.parameters(recurse=True):
+                prm.grad = None
+        ref.add_module(name, c)
+    ref.train(model.training)
+    return ref.__dict__.copy()
+
+
+class ReferencePickle:
+    """``torch.save(ReferencePickle(model), path)`` writes the whole-module pickle the reference's
+    ``torch.save(model)`` writes (utils/training_tools.py:49): loading it rebuilds the LOADER's
+    ``utils.models.smallcnn`` -- the reference's class for its defenses (fp.py:125 then hooks and
+    ``prune.custom_from_mask`` its submodules, fp.py:137,171; ft_reg.py:238, tsbd.py:256,
+    correlation_analysis.py:128), this package's drop-in under ``abd_amd.run`` (flowmur.py:55) --
+    with nothing of abd_amd needed to unpickle it."""
+
+    def __init__(self, model: smallcnn, module: str = "utils.models", name: str = "smallcnn"):
+        self.model, self.module, self.name = model, module, name
+
+    def __reduce_ex__(self, protocol):
+        return (copyreg._reconstructor, (_ClassRef(self.module, self.name), object, None),
+                reference_module_state(self.model))
+
+
+def save_reference_checkpoint(model, path):
+    """torch.save in the reference's format: abd smallcnn -> a utils.models.smallcnn pickle; any other
+    module is saved as is (the reference's behaviour)."""
+    torch.save(ReferencePickle(model) if isinstance(model, smallcnn) else model, path)
+
+
 class EarlyStoppingModel:
     """utils/training_tools.py:4-50 (patience on the monitored loss, whole-module checkpoint on improvement).
 
@@ -282,5 +346,5 @@ class EarlyStoppingModel:
     def save_checkpoint(self, val_loss, model):
         if self.verbose:
             self.trace_func(f"Validation loss decreased ({self.val_loss_min:.4f} --> {val_loss:.4f}).  Saving model ...")
-        torch.save(model, self.path)
+        save_reference_checkpoint(model, self.path)
         self.val_loss_min = val_loss

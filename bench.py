@@ -25,7 +25,9 @@ sys.path.insert(0, HERE)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec; 155 measured)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense ~2.5 PF (no sparsity)
-BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad")  # smallcnn GEMMs the bf16 modes move
+# smallcnn GEMMs the bf16 / f32split modes run on bf16 MFMA (the weight gradients through
+# conv_wgrad_trp_kernel: six split terms in f32split, one bf16 term in bf16)
+BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad", "conv2_wgrad", "conv3_wgrad")
 SPLIT_TERMS = 6                 # f32split: six bf16 MFMA terms per fp32-accurate product
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -56,10 +58,13 @@ def algorithmic_work(phase, B, H0, W0, K, n_mels, T, C, L):
         # wave read + mel-dB workspace write (trigger/tables amortised)
         "stft_mel": B * (4.0 * L + 4.0 * T * n_mels),
         "db_dct": B * (4.0 * T * n_mels + 4.0 * T * C),
-        "bn2_bwd": B * H2 * W2 * 64 * 4.0 * 3,   # r2 (stats) + r2 read + dz2 write
-        "bn2_pool": B * (H2 * W2 + H2p * W2p) * 64 * 4.0,
-        "conv1_bwd_wgrad": B * (H0 * W0 + H1 * W1p * 64) * 4.0,
+        # bn_bwd_apply_kernel: r2 read + pooled gradient dp2 read + dz2 write (the statistics pass
+        # over r2 left the step in round 2: BN2's sums are derived from conv3's gradients)
+        "bn2_bwd": B * (2.0 * H2 * W2 + H2p * W2p) * 64 * 4.0,
+        "bn2_pool": B * (H2 * W2 + H2p * W2p) * 64 * 4.0,        # r2 read + p2 write
+        "conv1_bwd_wgrad": B * (H0 * W0 + H1 * W1p * 64) * 4.0,   # x read + dp1 read
         "conv1_bn_pool": B * (H0 * W0 + H1 * W1p * 64) * 4.0,
+        "conv1_stats": B * (H0 * W0 + H1 * W1p * 64) * 4.0,       # x read + pool1-selected m write (fold)
     }
     if phase in by:
         return by[phase] / 1e9, "GB/s", "hbm"
@@ -97,17 +102,37 @@ def mfma_peak(phase, precision=None):
 _PRECISION = ["f32split"]
 
 
+_TRAFFIC = []
+
+
+def traffic_file():
+    """The committed rocprofv3 FETCH/WRITE measurement (profiles/*traffic*.json, scripts/traffic_json.py)
+    taken on THESE libabd sources (its csrc_sha1 equals theirs), newest first; None if there is none --
+    an older measurement of different kernels is never used."""
+    if not _TRAFFIC:
+        import glob
+        sys.path.insert(0, os.path.join(HERE, "scripts"))
+        from traffic_json import csrc_sha1
+        sha, found = csrc_sha1(HERE), None
+        for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*traffic*.json")), key=os.path.getmtime,
+                        reverse=True):
+            try:
+                d = json.load(open(f))
+            except Exception:
+                continue
+            if d.get("csrc_sha1") == sha:
+                found = (os.path.relpath(f, HERE), d)
+                break
+        _TRAFFIC.append(found)
+    return _TRAFFIC[0]
+
+
 def load_traffic(phase):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*traffic*.json), if any."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*traffic*.json")), reverse=True):
-        try:
-            d = json.load(open(f))
-            if phase in d.get("bytes_per_launch", {}):
-                return d["bytes_per_launch"][phase]
-        except Exception:
-            pass
-    return None
+    """(HBM bytes per launch, source file) for a phase from the same-source traffic file, else (None, None)."""
+    tf = traffic_file()
+    if tf is None or phase not in tf[1].get("bytes_per_launch", {}):
+        return None, None
+    return tf[1]["bytes_per_launch"][phase], tf[0]
 
 
 def cpu_threads():
@@ -303,17 +328,18 @@ def main():
             if dominant in FEATURE_PHASES:
                 amount = args.batch * feature_bytes(L_, T, C) / 1e9
                 unit, bound, peak = "GB/s", "hbm", HBM_PEAK_GBPS
-                traffic = None
+                traffic, tsrc = None, None
                 if headline:
                     tb = [load_traffic(ph) for ph in live]
-                    traffic = sum(tb) if all(v is not None for v in tb) else None
+                    if all(v is not None for v, _ in tb):
+                        traffic, tsrc = sum(v for v, _ in tb), tb[0][1]
             else:
                 amount, unit, bound = algorithmic_work(dominant, args.batch, T, C, K, 128, T, C, L_)
                 peak = mfma_peak(dominant) if bound == "mfma" else HBM_PEAK_GBPS
-                traffic = load_traffic(dominant) if headline else None
+                traffic, tsrc = load_traffic(dominant) if headline else (None, None)
             achieved = amount / avg_s
             roof = {"kernel": "+".join(live), "bound": bound, "achieved": round(achieved, 3), "peak": peak,
-                    "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes": round(amount * 1e9) if unit == "GB/s" else None,
                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
                     "formula": ("B*(4L + 4*T*C) / (avg stft_mel + avg db_dct) [SURVEY 8d feature bytes]"
@@ -341,8 +367,9 @@ def main():
             amt, unit, bnd = wk
             ach = amt / (pms / pcnt / 1e3)
             pk = mfma_peak(ph) if bnd == "mfma" else HBM_PEAK_GBPS
-            per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "frac": round(ach / pk, 4),
-                              "ms": round(pms / pcnt, 4), "traffic": load_traffic(ph) if headline else None}
+            tb, tsrc = load_traffic(ph) if headline else (None, None)
+            per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "peak": pk, "frac": round(ach / pk, 4),
+                              "ms": round(pms / pcnt, 4), "traffic": tb, "traffic_source": tsrc}
         cpu = None
         if world == 1 and not args.no_cpu and args.cpu_steps > 0 and args.attack == "ultrasonic":
             cpu = cpu_baseline(args.batch, cpu_threads(), args.cpu_steps)

@@ -238,7 +238,8 @@ int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const c
 int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch);
 
 /* Device-side counters written by the train/eval launches (int64 / double):
- *   [0] sum of per-batch mean losses (double bits)  [1] samples  [2] correct
+ *   [0] sum of per-batch mean losses (double bits; train steps weight each by
+ *       grad_scale)  [1] samples  [2] correct
  *   [3] poisoned samples  [4] poisoned & predicted==label  [5] batches     */
 #define ABD_METRICS_WORDS 8
 
@@ -262,7 +263,12 @@ typedef struct abd_train_args {
   uint8_t* mask2_out;
   float* logprobs_out;       /* optional (B,K)                                */
   int64_t* metrics;          /* ABD_METRICS_WORDS accumulators (device)       */
-  float grad_scale;          /* multiply loss gradient (DP: local/global)     */
+  float grad_scale;          /* multiply loss gradient (DP: B_local/B_global);
+                              * also weights metrics[0]'s batch-mean loss, so
+                              * the ranks' words sum to the global batch mean
+                              * (uneven last batch included).  batch >= 1:
+                              * a 1-row batch is valid (BatchNorm2d counts
+                              * N*H*W elements per channel)                  */
   int64_t* num_batches_tracked; /* optional int64[3] (bn1..bn3), += 1          */
   void* fc_grads_event;      /* optional hipEvent_t, recorded on the stream once
                               * the fc1/fc2 gradients (flat tail from offset

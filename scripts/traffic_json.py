@@ -1,33 +1,71 @@
-"""HBM bytes per launch for the bench phases from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
+"""HBM bytes per launch of the bench phases from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
     python scripts/traffic_json.py gpurun_out/<tag> profiles/<name>_traffic.json
 
-Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it is
-doubled; WRITE_SIZE is exact for 16-B stores.  The last dispatch of each kernel in the
-profiled bench run is used (steady state).  Kernels shared by two phases (gemm_nt<64,0>
-runs conv3 then conv2 data gradients) resolve to the later one, conv2.  A phase lists the
-fp32 kernel and the f32split kernel; the profiled run uses one of them.
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it is doubled; WRITE_SIZE
+is exact for 16-B stores.
+
+Kernels are matched by their EXACT name (template arguments included, argument list dropped) and,
+for a kernel that runs more than once per step (bn_bwd_apply_kernel: BN3 then BN2), by its
+occurrence within the LAST step of the profiled run (the dispatches after the last STFT launch).
+The output records the sha1 of the libabd sources it was measured on (``csrc_sha1``): bench.py
+only uses a traffic file whose hash matches the sources it runs, and names that file per phase.
 """
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
+import re
 import sys
 
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# phase -> candidate (exact kernel, occurrence within one step); the first candidate present is used
 PHASE_KERNELS = {
-    "stft_mel": "stft_mel_fast_kernel<2304, 1103",
-    "db_dct": ("db_dct_lds_kernel", "db_dct_mfma_kernel"),
-    "conv2_fwd": ("gemm_nt_kernel<64, 1, 1>", "gemm_nt_bf16_kernel<64, 1, 32, 3, 1>", "conv_ws_split_kernel<1"),
-    "conv2_dgrad": ("gemm_nt_kernel<64, 0, 1>", "gemm_nt_bf16_kernel<64, 0, 32, 3, 1>", "conv_ws_split_kernel<0"),
-    "conv2_wgrad": "conv_wgrad_rows_kernel<64, 64>",
-    "conv1_bwd_wgrad": "conv1_wgrad_kernel",
-    "bn2_bwd": "bn_bwd_apply_kernel",
+    "stft_mel": [("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
+    "db_dct": [("db_dct_mfma_kernel<3>", 0)],
+    "conv1_stats": [("conv1_stats_fold_kernel", 0), ("conv1_stats_kernel", 0)],
+    "conv2_fwd": [("conv_ws_split_kernel<1, 2, 64, 1, 8, 8>", 0), ("conv_ws_kernel<1, 2, 64, 1, 8, 8>", 0)],
+    "bn2_pool": [("bn_pool_fwd_kernel", 0)],
+    "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8>", 0), ("conv_ws_kernel<1, 1, 64, 1, 4, 8>", 0)],
+    "bn3_pool_dropout": [("bn_pool_fwd_kernel", 1)],
+    "fc_head": [("fc_head_kernel", 0)],
+    "fc1_fwd": [("gemm_nt_kernel<128, 4, 1, 32>", 0)],
+    "fc1_wgrad": [("gemm_tn_kernel<128, 128>", 0)],
+    "fc1_dgrad": [("gemm_nt_kernel<32, 3, 1, 32>", 0)],
+    "bn3_bwd": [("bn_bwd_apply_kernel", 0)],
+    "conv3_wgrad": [("conv_wgrad_trp_kernel<4, 32, 2, 4>", 0)],
+    "conv3_dgrad": [("conv_ws_split_kernel<0, 2, 32, 1, 4, 8>", 0), ("conv_ws_kernel<0, 2, 32, 1, 4, 8>", 0)],
+    "bn2_bwd": [("bn_bwd_apply_kernel", 1)],
+    "conv2_wgrad": [("conv_wgrad_trp_kernel<6, 64, 5, 11>", 0)],
+    "conv2_dgrad": [("conv_ws_split_kernel<0, 2, 64, 1, 8, 8>", 0), ("conv_ws_kernel<0, 2, 64, 1, 8, 8>", 0)],
+    "conv1_bwd_wgrad": [("conv1_wgrad_kernel<true>", 0)],
 }
+STEP_START = "stft_mel_fast_kernel<"
 
 
-def last_dispatch(d, counter):
-    out = {}
+def csrc_sha1(root=HERE):
+    """sha1 over libabd's sources (name + bytes, sorted): identifies the code a measurement belongs to."""
+    h = hashlib.sha1()
+    d = os.path.join(root, "audio-backdoor-attack_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
+def kernel_key(name):
+    k = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return k[:k.index("(")] if "(" in k else k
+
+
+def last_step(d, counter):
+    """[(kernel key, value)] of the dispatches after the last STFT launch, in dispatch order."""
+    rows = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         agg = collections.defaultdict(float)
         name = {}
@@ -36,27 +74,36 @@ def last_dispatch(d, counter):
                 continue
             did = int(r["Dispatch_Id"])
             agg[did] += float(r["Counter_Value"])
-            name[did] = r["Kernel_Name"]
-        for did in sorted(agg):
-            out[name[did]] = agg[did]
-    return out
+            name[did] = kernel_key(r["Kernel_Name"])
+        rows += [(did, name[did], agg[did]) for did in agg]
+    rows.sort()
+    starts = [i for i, (_, k, _) in enumerate(rows) if k.startswith(STEP_START)]
+    if not starts:
+        return []
+    return [(k, v) for _, k, v in rows[starts[-1]:]]
+
+
+def pick(step, cands):
+    for key, occ in cands:
+        hits = [v for k, v in step if k == key]
+        if len(hits) > occ:
+            return key, occ, hits[occ]
+    return None
 
 
 def main():
     d, dst = sys.argv[1], sys.argv[2]
-    fetch = last_dispatch(d, "FETCH_SIZE")
-    write = last_dispatch(d, "WRITE_SIZE")
-    res = {"source": d, "correction": "FETCH_SIZE x2 (gfx950 wide reads), KiB -> bytes", "bytes_per_launch": {},
+    fetch, write = last_step(d, "FETCH_SIZE"), last_step(d, "WRITE_SIZE")
+    res = {"source": d, "csrc_sha1": csrc_sha1(),
+           "correction": "FETCH_SIZE x2 (gfx950 wide reads), KiB -> bytes; last profiled step", "bytes_per_launch": {},
            "detail": {}}
-    for ph, subs in PHASE_KERNELS.items():
-        subs = subs if isinstance(subs, tuple) else (subs,)   # fp32 kernel, f32split kernel
-        fk = [v for k, v in fetch.items() if any(x in k for x in subs)]
-        wk = [v for k, v in write.items() if any(x in k for x in subs)]
-        if not fk or not wk:
+    for ph, cands in PHASE_KERNELS.items():
+        f, w = pick(fetch, cands), pick(write, cands)
+        if f is None or w is None:
             continue
-        rb, wb = 2 * fk[-1] * 1024, wk[-1] * 1024
+        rb, wb = 2 * f[2] * 1024, w[2] * 1024
         res["bytes_per_launch"][ph] = round(rb + wb)
-        res["detail"][ph] = {"read_bytes": round(rb), "write_bytes": round(wb)}
+        res["detail"][ph] = {"kernel": f[0], "occurrence": f[1], "read_bytes": round(rb), "write_bytes": round(wb)}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res["bytes_per_launch"]))
 

@@ -52,14 +52,103 @@ def test_state_dict_loads_into_reference_smallcnn(K, lf):
         assert torch.allclose(ref(x), t(x), rtol=1e-5, atol=1e-5)
 
 
-def test_whole_module_checkpoint_round_trip(tmp_path):
-    m = _model()
+def _write_checkpoint(tmp_path, K=10, lf=3072):
+    m = _model(K, lf)
+    m.eval()
     es = EarlyStoppingModel(patience=2, verbose=False, path=str(tmp_path / "checkpoint.pt"))
     es(1.0, m)      # first call always saves (training_tools.py:31-33)
     es(1.5, m)      # no improvement: counter 1
     es(2.0, m)      # counter 2 -> early stop
     assert es.early_stop and es.counter == 2
-    loaded = torch.load(str(tmp_path / "checkpoint.pt"), weights_only=False)   # written by this test
-    assert isinstance(loaded, smallcnn) and loaded._engine is None
+    return m, str(tmp_path / "checkpoint.pt")
+
+
+def test_whole_module_checkpoint_round_trip(tmp_path):
+    """Under the drop-in (abd_amd.run puts dropin/ first: flowmur.py:55 reloads its benign model),
+    the pickle resolves utils.models.smallcnn to the accelerated class."""
+    m, path = _write_checkpoint(tmp_path)
+    dropin = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          "audio-backdoor-attack_amd", "dropin")
+    saved = {k: v for k, v in sys.modules.items() if k == "utils" or k.startswith("utils.")}
+    for k in saved:
+        del sys.modules[k]
+    sys.path.insert(0, dropin)
+    try:
+        loaded = torch.load(path, weights_only=False)   # written by this test
+    finally:
+        sys.path.remove(dropin)
+        for k in [k for k in sys.modules if k == "utils" or k.startswith("utils.")]:
+            del sys.modules[k]
+        sys.modules.update(saved)
+    assert isinstance(loaded, smallcnn) and loaded._engine is None and loaded._step == 0
+    assert loaded.gemm_precision == "f32" and not loaded.training
     a, b = m.state_dict(), loaded.state_dict()
     assert sorted(a) == sorted(b) and all(torch.equal(a[k], b[k]) for k in a)
+
+
+_CONSUMER = r"""
+import sys, json
+sys.dont_write_bytecode = True
+sys.path[:] = [p for p in sys.path if p and 'repo' not in p]
+sys.path.insert(0, {ref!r})
+import torch, torch.nn as nn
+from torch.nn.utils import prune
+m = torch.load({path!r}, map_location='cpu', weights_only=False)   # fp.py:125 (our own file)
+out = {{"module": type(m).__module__, "cls": type(m).__name__,
+        "abd_loaded": any(k.startswith('abd_amd') for k in sys.modules)}}
+m.eval()
+m.requires_grad_(False)
+import copy
+mc = copy.deepcopy(m)                                              # fp.py:128
+name, last = list(mc.named_children())[-1]                         # fp.py:137
+out["last_child"] = name
+fired = []
+h = mc.fc2.register_forward_hook(lambda mod, i, o: fired.append(tuple(i[0].shape)))
+x = torch.load({xpath!r}, weights_only=True)
+with torch.no_grad():
+    y = mc(x)
+out["hook"] = fired
+h.remove()
+mask = torch.ones_like(mc.fc1.weight)
+mask[:, :7] = 0
+prune.custom_from_mask(mc.fc1, name="weight", mask=mask)          # fp.py:171
+with torch.no_grad():
+    yp = mc(x)
+out["pruned_has_orig"] = hasattr(mc.fc1, "weight_orig")
+torch.save({{"y": y, "yp": yp}}, {ypath!r})
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "utils")), reason="reference checkout not present")
+@pytest.mark.parametrize("K,lf,H,W", [(10, 3072, 101, 40), (35, 3072, 100, 40), (10, 896, 32, 40)])
+def test_checkpoint_loads_as_reference_class_without_abd(tmp_path, K, lf, H, W):
+    """the defenses (fp.py, ft_reg.py, tsbd.py, correlation_analysis.py) torch.load the
+    checkpoint with only the reference on sys.path and operate on its submodules."""
+    import json
+    import subprocess
+    m, path = _write_checkpoint(tmp_path, K, lf)
+    torch.manual_seed(3)
+    x = torch.randn(4, 1, H, W) * 20
+    xpath, ypath = str(tmp_path / "x.pt"), str(tmp_path / "y.pt")
+    torch.save(x, xpath)
+    code = _CONSUMER.format(ref=REF, path=path, xpath=xpath, ypath=ypath)
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    env["PYTHONDONTWRITEBYTECODE"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=str(tmp_path),
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["module"] == "utils.models" and out["cls"] == "smallcnn" and not out["abd_loaded"], out
+    assert out["last_child"] == "softmax"                 # the reference's own child order
+    assert out["hook"] == [[4, 128]] and out["pruned_has_orig"], out
+    ys = torch.load(ypath, weights_only=True)
+    t = torch_ref.SmallCNN(K, lf)
+    t.load_state_dict(m.state_dict(), strict=True)
+    t.eval()
+    with torch.no_grad():
+        exp = t(x)
+        t.fc1.weight[:, :7] = 0
+        exp_p = t(x)
+    assert torch.allclose(ys["y"], exp, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(ys["yp"], exp_p, rtol=1e-5, atol=1e-5)

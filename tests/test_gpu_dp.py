@@ -176,3 +176,74 @@ def test_two_rank_sync_bn_step_equals_one_rank_step():
         if rank == 0:
             assert r["params"] < 1e-5 and r["running"] < 1e-5, r
             assert r["loss"] < 1e-5 and r["acc"][0] == r["acc"][1] and r["samples"][0] == r["samples"][1], r
+
+
+def _tail_worker(rank, world, port, q, N):
+    """A full epoch of N rows (not a multiple of the global batch) on the daba geometry (32x40 Slaney
+    front end, fc 896): 2 ranks x 32 with SyncBN vs 1 rank x 64; the last batch is kept
+    (drop_last=False, daba.py:152-154) and split unevenly -- for N % 64 == 1 rank 1 has no rows."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import torch.distributed as dist
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import abd_amd
+        from abd_amd import synth
+        from abd_amd.models import smallcnn
+        from abd_amd.pipeline import ResidentTrainer, attack_config
+        abd_amd.load_library()
+        cfg = attack_config("daba")
+        G, K = 64, 10
+        waves, labels = synth.make_clips_torch(N, cfg.sample_rate, cfg.length, K, seed=36, device=dev)
+
+        def run(world_, rank_):
+            torch.manual_seed(35)
+            model = smallcnn(K, cfg.linear_features).to(dev)
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+            tr = ResidentTrainer(cfg, waves, labels, model, opt, G // world_, seed=35, rank=rank_, world=world_,
+                                 sync_bn=world_ > 1)
+            steps = tr.steps_per_epoch()
+            m = tr.run_epoch()
+            tr.sync_buffers()
+            eng = model._engine
+            torch.cuda.synchronize()
+            return eng.params.clone(), eng.running.clone(), eng.nbt.clone(), m, steps, tr.adam.step
+
+        p2, r2, n2, m2, steps2, adam2 = run(world, rank)
+        res = None
+        if rank == 0:
+            p1, r1, n1, m1, steps1, adam1 = run(1, 0)
+            nrel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+            res = {"params": nrel(p2, p1), "running": nrel(r2, r1), "nbt": (n2.tolist(), n1.tolist()),
+                   "loss": abs(m2["loss"] - m1["loss"]) / m1["loss"], "acc": (m2["acc"], m1["acc"]),
+                   "samples": (m2["samples"], m1["samples"]), "steps": (steps2, steps1), "adam": (adam2, adam1)}
+        q.put((rank, res, None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("N", [230, 193])
+def test_two_rank_uneven_tail_epoch_equals_one_rank(N):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tail_worker, args=(r, 2, port, q, N)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=110) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    for rank, r, tb in res:
+        assert tb is None, tb
+        if rank == 0:
+            assert r["steps"] == (4, 4) and r["adam"] == (4, 4), r
+            assert r["samples"] == (N, N), r
+            assert r["params"] < 1e-5 and r["running"] < 1e-5 and r["loss"] < 1e-5, r
+            assert r["acc"][0] == r["acc"][1] and r["nbt"][0] == r["nbt"][1], r

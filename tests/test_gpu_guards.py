@@ -65,10 +65,10 @@ def test_mfcc_stays_inside_workspace_and_output(dev, name):
             inj = F.Injection(mode=cfg.inject_mode, trigger=trig,
                               poison=(torch.arange(B, device=dev) % 3 == 0).to(torch.uint8))
         need = L.lib().abd_mfcc_workspace_bytes(plan._h, B)
-        plan._ws = torch.full((need + GUARD,), PAT, dtype=torch.uint8, device=dev)
+        ws = torch.full((need + GUARD,), PAT, dtype=torch.uint8, device=dev)
         out = torch.full((B + 4, 1, plan.n_frames, cfg.n_mfcc), float("nan"), device=dev)
-        F.mfcc_batch(waves, mc, rows=rows, inject=inj, out=out[:B])
+        F.mfcc_batch(waves, mc, rows=rows, inject=inj, out=out[:B], workspace=ws)
         torch.cuda.synchronize()
-        assert int((plan._ws[need:] != PAT).sum().item()) == 0, (name, B)
+        assert int((ws[need:] != PAT).sum().item()) == 0, (name, B)
         assert torch.isnan(out[B:]).all(), (name, B)   # rows past the batch untouched
         assert torch.isfinite(out[:B]).all()

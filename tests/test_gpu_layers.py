@@ -28,7 +28,7 @@ def ws_view(eng, ws, B, name, shape, dtype=torch.float32):
 
 
 @pytest.mark.parametrize("prec", ["f32", "f32split"])
-@pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 48)])
+@pytest.mark.parametrize("shape", [(101, 40, 10, 64), (32, 13, 10, 48), (32, 40, 10, 1)])
 def test_every_buffer_matches_oracle(shape, prec):
     """prec 'f32split' also covers the train step's BN1 fold into conv2 (conv1_stats_fold_kernel)."""
     assert torch.cuda.is_available()
