@@ -1852,16 +1852,41 @@ __device__ __forceinline__ void split3_x8(const float4& lo, const float4& hi, bf
   for (int q = 0; q < 3; ++q) pl[q] = __builtin_bit_cast(bf16x8, make_uint4(u[q][0], u[q][1], u[q][2], u[q][3]));
 }
 
+// NP = 1 (ABD_PREC_BF16): one plane, the operands rounded to bf16 (RNE) and ONE MFMA term a0 b0
+// per step -- the same weight-stationary schedule at a sixth of the MFMA work.
+__device__ __forceinline__ void round1_x8(const float4& lo, const float4& hi, bf16x8* pl) {
+  const f32x2 in[4] = {f32x2{lo.x, lo.y}, f32x2{lo.z, lo.w}, f32x2{hi.x, hi.y}, f32x2{hi.z, hi.w}};
+  uint32_t u[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(in[h], bf16x2));
+  pl[0] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+}
+template <int NP>
+__device__ __forceinline__ void planes_x8(const float4& lo, const float4& hi, bf16x8* pl) {
+  if constexpr (NP == 3) split3_x8(lo, hi, pl);
+  else round1_x8(lo, hi, pl);
+}
+// MFMA terms (a plane, b plane) of a product: six for the exact 3-plane split, one for bf16
+template <int NP> struct Terms;
+template <> struct Terms<3> {
+  static constexpr int n = 6;
+  static constexpr int A[6] = {2, 0, 1, 1, 0, 0}, B[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
+};
+template <> struct Terms<1> {
+  static constexpr int n = 1;
+  static constexpr int A[1] = {0}, B[1] = {0};
+};
+
 // Template parameters: NJ = N / 32 output-channel tiles, CS = input channels (K = 4 CS), MI = 32-row
 // A fragments per wave tile, PDW = K steps the A loads run ahead (register ring of PDW slots),
-// WPB = waves per block.  conv2: <2, 64, 2> (101 KB of weights, one 8-wave block per CU);
-// conv3 forward <1, 64, 1> and data gradient <2, 32, 1> (48 KB, smaller tiles for their
-// 150-180 k rows).
-template <int EPI, int NJ, int CS, int MI, int PDW, int WPB>
+// WPB = waves per block, NP = bf16 planes per operand (3: f32split, 1: bf16).  conv2: <2, 64, 2>
+// (101 KB of weights, one 8-wave block per CU); conv3 forward <1, 64, 1> and data gradient
+// <2, 32, 1> (48 KB, smaller tiles for their 150-180 k rows).
+template <int EPI, int NJ, int CS, int MI, int PDW, int WPB, int NP = 3>
 __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   constexpr int N = 32 * NJ, K = 4 * CS, LD = K + 8, KS = K / 16, TR = 32 * MI;
   static_assert(KS % PDW == 0, "a tile's K steps must be a whole number of ring turns");
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][N * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
   __shared__ float red[WPB][N][2];
   __shared__ float bfold[N];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1870,10 +1895,10 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
     const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
     const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
     const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
-    bf16x8 pl[3];
-    split3_x8(lo, hi, pl);
+    bf16x8 pl[NP];
+    planes_x8<NP>(lo, hi, pl);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
+    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
   }
   if (EPI == EPI_CONV && a.fold_t != nullptr) {
     // folded bias b_n + sum_c ft[c][n] (bn_finalize_kernel), 8 lanes per output channel; a.Bw holds
@@ -1953,34 +1978,34 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
     f32x16 acc[MI][NJ];
     // B fragments of a K step (identical for every tile), double-buffered: step ks's MFMAs use
     // bvs[ks & 1] while the reads for step ks + 1 are in flight (LDS latency off the MFMA path)
-    bf16x8 bvs[2][NJ][3];
-    auto load_b = [&](int ks, bf16x8 (&bv)[NJ][3]) {
+    bf16x8 bvs[2][NJ][NP];
+    auto load_b = [&](int ks, bf16x8 (&bv)[NJ][NP]) {
       const int kb = ks * 16 + kq;  // k = tap * CS + channel, 16 per step
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NP; ++q)
           bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
     };
     auto step = [&](int ks, float4 (&r)[MI][2], const RowInfo& li, int lks) {
-      bf16x8 av[MI][3];
-      bf16x8 (&bv)[NJ][3] = bvs[ks & 1];
+      bf16x8 av[MI][NP];
+      bf16x8 (&bv)[NJ][NP] = bvs[ks & 1];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) split3_x8(r[i][0], r[i][1], av[i]);
+      for (int i = 0; i < MI; ++i) planes_x8<NP>(r[i][0], r[i][1], av[i]);
       // keep the refill behind the split: hoisted above it, the loads need fresh registers and
       // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
       __builtin_amdgcn_sched_barrier(0);
       load(li, lks, r);  // unconditional: a conditional refill is a phi (copies)
       load_b((ks + 1) % KS, bvs[(ks + 1) & 1]);
       // term-major: independent accumulator chains between dependent MFMAs
-      constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
 #pragma unroll
-      for (int term = 0; term < 6; ++term)
+      for (int term = 0; term < Terms<NP>::n; ++term)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]],
+                                                                acc[i][j], 0, 0, 0);
     };
     RowInfo li = rows_of(r_lo);
     // in step order: the scheduler otherwise issues them last-slot-first, slot 0 becomes the
@@ -2706,7 +2731,9 @@ __global__ void __launch_bounds__(kT, NBUF == 1 ? 3 : 2) conv_wgrad_tr_kernel(WG
 #ifndef ABD_TRP_ABL  // ablation bits (measurement builds): 1 no MFMAs, 2 no staging writes, 4 no loads
 #define ABD_TRP_ABL 0
 #endif
-template <int R, int NB, int NS, int MAXS>
+// NP = 1 (ABD_PREC_BF16): one RNE-rounded bf16 plane per operand and one MFMA term (a0 b0); the
+// staging of chunk c + 1 then rides on each step's single term.
+template <int R, int NB, int NS, int MAXS, int NP = 3>
 __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
   constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4, Qd = 16 * NS;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
@@ -2767,12 +2794,12 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
     if constexpr (ABD_TRP_ABL & 2) return;
     f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < NP; ++pl) {
       uint32_t u[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x[h], bf16x2));
-        if (pl < 2) {
+        if (pl < NP - 1) {
           const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
           x[h] -= back;
         }
@@ -2790,25 +2817,26 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
   };
   const int toff = (wave >> 1) * Ws + (wave & 1);
   struct Frags {
-    bf16x8 av[NT][3], bv[2][3];
+    bf16x8 av[NT][NP], bv[2][NP];
   };
   auto load_frags = [&](const unsigned char* cur, int s, Frags& F) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < NP; ++pl) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) F.av[t][pl] = frag(cur, 16 * s, t, pl);
 #pragma unroll
       for (int t = 0; t < 2; ++t) F.bv[t][pl] = frag(cur + Qd * kTrRow, 16 * s + toff, t, pl);
     }
   };
-  constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
+  constexpr int NTERM = Terms<NP>::n;
   auto term = [&](const Frags& F, int tm) {
     if constexpr (ABD_TRP_ABL & 1) return;
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.av[i][TA[tm]], F.bv[j][TB[tm]], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.av[i][Terms<NP>::A[tm]], F.bv[j][Terms<NP>::B[tm]],
+                                                            acc[i][j], 0, 0, 0);
   };
   // chunk c from `cur`; chunk c + 1's registers stP -> `nxt`; chunk c + 2 -> stF
   auto body = [&](int c, const unsigned char* cur, unsigned char* nxt, const float4 (&stP)[MAXS],
@@ -2827,12 +2855,18 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       if (s + 1 < NS) load_frags(cur, s + 1, F[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NTERM == 1) {
 #pragma unroll
-      for (int tm = 1; tm < 6; ++tm) {
-        term(F[s & 1], tm);
+        for (int k = 0; k < MAXS; ++k)  // slot k rides on step k % NS
+          if (k % NS == s) put_slot(k, stP[k], nxt);
+      } else {
 #pragma unroll
-        for (int k = 0; k < MAXS; ++k)  // slot k rides on step k % NS, term 1 + (k / NS) % 5
-          if (k % NS == s && 1 + (k / NS) % 5 == tm) put_slot(k, stP[k], nxt);
+        for (int tm = 1; tm < NTERM; ++tm) {
+          term(F[s & 1], tm);
+#pragma unroll
+          for (int k = 0; k < MAXS; ++k)  // slot k rides on step k % NS, term 1 + (k / NS) % 5
+            if (k % NS == s && 1 + (k / NS) % (NTERM - 1) == tm) put_slot(k, stP[k], nxt);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -3406,7 +3440,7 @@ int launch_wgrad_tr_n(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 // conv_wgrad_trp_kernel<R, NB, NS, MAXS> launch; -1 when the geometry is not this instantiation's
-template <int R, int NB, int NS, int MAXS>
+template <int R, int NB, int NS, int MAXS, int NP = 3>
 int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                        float* slab, int phase, hipStream_t s) {
   if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
@@ -3425,7 +3459,7 @@ int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs
   a.slab = slab;
   const size_t lds = 2 * (size_t)(Qd + Qs + 1) * kTrRow;
   if (lds > 160 * 1024) return -1;
-  auto* kern = &conv_wgrad_trp_kernel<R, NB, NS, MAXS>;
+  auto* kern = &conv_wgrad_trp_kernel<R, NB, NS, MAXS, NP>;
   static size_t cached = 0;
   static int per_cu = 1, n_cu = 256;
   if (cached != lds) {
@@ -3448,25 +3482,25 @@ int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs
   return grid;
 }
 
-template <int R, int NB>
+template <int R, int NB, int NP = 3>
 int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                     float* slab, int phase, hipStream_t s) {
   static const bool trp = env_int("ABD_WGRAD_TRP", 1) != 0;
-  if (trp) {
+  if (trp || NP == 1) {
     int r = -1;
     // conv2 at W = 40 (Ws = 13): 6-row chunks fill 72 of 80 staged positions (2-row: 24 of 32)
     static const int r6 = env_int("ABD_WGRAD_TRP_R6", 1);
     if constexpr (NB == 64) {
-      if (r6) r = launch_wgrad_trp_n<6, NB, 5, 11>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 2, 5>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 8>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 4>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r6) r = launch_wgrad_trp_n<6, NB, 5, 11, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 2, 5, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 8, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
     } else {
-      r = launch_wgrad_trp_n<R, NB, 2, 4>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 6>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 2>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      r = launch_wgrad_trp_n<R, NB, 2, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 6, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 2, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
     }
-    if (r >= 0) return r;
+    if (r >= 0 || NP == 1) return r;
   }
   static const int nbuf = env_int("ABD_WGRAD_TR_BUF", 2);
   return nbuf == 2 ? launch_wgrad_tr_n<R, NB, 2>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s)
@@ -3573,7 +3607,7 @@ int ws_blocks(int N, int Cs) {
   static const int m3 = std::max(1, env_int("ABD_WS3_MULT", 1));
   return (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
 }
-template <int EPI>
+template <int EPI, int NP = 3>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
   const int nb = ws_blocks(a.N, a.Cs);
@@ -3581,11 +3615,11 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
   static const int cfg = env_int("ABD_WS_CFG", 2);  // conv2 tile / ring / waves-per-block (A/B knob)
-  if (a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16><<<dim3(nb), dim3(1024), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 64 && cfg == 2) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 32) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8><<<dim3(nb), dim3(512), 0, s>>>(a);
+  if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 64 && (cfg == 2 || NP == 1)) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (NP == 3 && a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 32) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
   else {
     if (phase >= 0) abd::prof_end(phase, s);
     return -1;
@@ -3834,9 +3868,9 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
-    const bool ws = sp && ws_on();
-    a.nblk = bf ? (a.M + kBM - 1) / kBM
-             : ws ? ws_blocks(64, 64)
+    const bool ws = (sp || bf) && ws_on();  // bf16: the same weight-stationary kernel on one plane
+    a.nblk = ws ? ws_blocks(64, 64)
+             : bf ? (a.M + kBM - 1) / kBM
              : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
              : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
@@ -3847,8 +3881,9 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
       a.fold_t = w.ft2;
     }
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
-    if (bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
-           : ws ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD)
+    if (ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
+                 : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+           : bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
            : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
                    : launch_conv_halo_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD) == 0
                        ? 0
@@ -3881,11 +3916,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
-    const bool ws3 = sp3 && ws_on();
+    const bool ws3 = (sp3 || bf3) && ws_on();
     a.nblk = ws3 ? ws_blocks(32, 64) : (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (bf3   ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD)
-        : ws3 ? launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD)
+    if (ws3   ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
+                     : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))
+        : bf3 ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD)
         : sp3 ? launch_nt_bf16<32, EPI_CONV, 32, 3>(a, s, abd::PH_CONV3_FWD)
               : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
       return -1;
@@ -3974,7 +4010,8 @@ bool bn_bwd_derived_on() {
 // conv1_bn_pool pass) when conv2's forward runs on the weight-stationary split kernel.
 bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
   static const bool on = env_int("ABD_BN1_FOLD", 1) != 0;
-  return on && net->precision == ABD_PREC_F32_SPLIT && ws_on() && split_mi() == 1 &&
+  return on && (net->precision == ABD_PREC_F32_SPLIT || net->precision == ABD_PREC_BF16) && ws_on() &&
+         split_mi() == 1 &&
          (int64_t)g.H1 * g.W1p * 64 * 4 * B < 0x7ffffff0LL;
 }
 // Stream for the conv weight gradients: they depend only on dz and the stored forward activations and
@@ -4147,7 +4184,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw3 = env_int("ABD_WGRAD_TR", 1) != 0;
-    int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw3 && !spw)
+    int nsl = net->precision == ABD_PREC_BF16
+                  ? launch_wgrad_tr<4, 32, 1>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
+                                              abd::PH_CONV3_WGRAD, sw)
+              : (net->precision == ABD_PREC_F32_SPLIT && trw3 && !spw)
                   ? (env_int("ABD_WGRAD_TR_R3", 4) == 2
                          ? launch_wgrad_tr<2, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
                                                   abd::PH_CONV3_WGRAD, sw)
@@ -4165,7 +4205,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                                 derive_fused ? &dv2 : nullptr))
       return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
-    if ((net->precision == ABD_PREC_BF16         ? launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD)
+    if ((net->precision == ABD_PREC_BF16
+             ? (launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV3_DGRAD) == 0
+                    ? 0
+                    : launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD))
         : net->precision == ABD_PREC_F32_SPLIT
             ? (launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD) == 0
                    ? 0
@@ -4208,7 +4251,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
-    int nsl = (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
+    int nsl = net->precision == ABD_PREC_BF16
+                  ? launch_wgrad_tr<2, 64, 1>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                              abd::PH_CONV2_WGRAD, sw)
+              : (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
                   ? (env_int("ABD_WGRAD_TR_R", 2) == 1
                          ? launch_wgrad_tr<1, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
                                                   abd::PH_CONV2_WGRAD, sw)
@@ -4226,7 +4272,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
-    if ((net->precision == ABD_PREC_BF16 ? launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD)
+    if ((net->precision == ABD_PREC_BF16
+             ? (launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV2_DGRAD) == 0
+                    ? 0
+                    : launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD))
         : net->precision == ABD_PREC_F32_SPLIT
             ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
                : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0 ? 0

@@ -84,7 +84,7 @@ def test_bf16_gemms_exact_on_rounded_operands(dev, shape, prec):
         # f32split train step: p1 holds m; conv2 runs on fl32(w * alpha_c) and bias b + sum w beta'_c
         # (conv1_stats_fold_kernel / conv_ws_split_kernel fold): the GEMM is checked on those operands
         c1 = ws_view(eng, ws, B, "coef", (3, 64, 4))[0]
-        w2f = (st["conv2.weight"].astype(np.float32) * c1[None, :, None, None, 2].astype(np.float32)).astype(np.float64)
+        w2f = rnd((st["conv2.weight"].astype(np.float32) * c1[None, :, None, None, 2].astype(np.float32)))
         b2 = (b2 + np.einsum("ncij,c->n", st["conv2.weight"].astype(np.float64), c1[:, 3])).astype(np.float32)
         p1_true = p1 * c1[:, 2] + c1[:, 3]
     ref_r2 = np.maximum(oc.conv2x2(rnd(nchw(p1)), w2f, b2.astype(np.float64)), 0.0)
@@ -93,9 +93,21 @@ def test_bf16_gemms_exact_on_rounded_operands(dev, shape, prec):
     ref_dp1, _, _ = oc.conv2x2_backward(np.zeros((B, 64, g["H1p"], g["W1p"])), w2, rnd(nchw(dz2)))
     errs = {"r2": nrel(nchw(r2), ref_r2), "r3": nrel(nchw(r3), ref_r3), "dp2": nrel(nchw(dp2), ref_dp2),
             "dp1": nrel(nchw(dp1), ref_dp1)}
-    print(shape, {k: f"{v:.1e}" for k, v in errs.items()})
+    # weight gradients (conv_wgrad_trp_kernel: six split terms / one bf16 term): the products of the
+    # same device operands, rounded; under the fold conv2's is taken over m and unfolded
+    # (alpha_c G_m + beta'_c db_n, slab_reduce_kernel)
+    grads = {n: v.cpu().numpy().astype(np.float64) for n, v in zip(M.PARAM_ORDER, eng.views(eng.grads))}
+    _, gw3, _ = oc.conv2x2_backward(rnd(nchw(p2)), w3, rnd(nchw(dz3)))
+    _, gw2, _ = oc.conv2x2_backward(rnd(nchw(p1)), w2, rnd(nchw(dz2)))
+    if folded:
+        gw2 = gw2 * c1[None, :, None, None, 2] + c1[None, :, None, None, 3] * grads["conv2.bias"][:, None, None, None]
+    wg = {"conv3.weight": nrel(grads["conv3.weight"].reshape(gw3.shape), gw3),
+          "conv2.weight": nrel(grads["conv2.weight"].reshape(gw2.shape), gw2)}
+    print(shape, prec, "folded" if folded else "", {k: f"{v:.1e}" for k, v in {**errs, **wg}.items()})
     for k, v in errs.items():
         assert v < 2e-6, (k, v)
+    for k, v in wg.items():
+        assert v < 1e-5, (k, v)
     # and the products really are bf16: the exact-fp32 product differs by ~bf16 rounding
     ref32 = np.maximum(oc.conv2x2(nchw(p1_true), st["conv2.weight"].astype(np.float64),
                                   st["conv2.bias"].astype(np.float64)), 0.0)
