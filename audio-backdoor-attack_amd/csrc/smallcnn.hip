@@ -3011,6 +3011,8 @@ __global__ void __launch_bounds__(kT) metrics_kernel(const float* rowinfo, int B
   metrics_body(rowinfo, B, metrics);
 }
 
+#include "fc_head.inc"
+
 // fc2 data gradient through dropout2/ReLU: da = (dz . W2) * scale2 * [d2 > 0]
 __device__ __forceinline__ void fc2_bwd_body(const float* dz, const float* d2, const float* w2, int B, int K,
                                              float scale2, float* da, int bx, int nb) {
@@ -3185,6 +3187,9 @@ struct Work {
   float *w2f, *w2d, *w3f, *w3d, *f1t;
   float* part;
   float *partb3, *partb2;  // BN3 / BN2 backward-apply bias partials (read by the side stream's slab reduction)
+  float* xh3;              // fused fc head: xhat of each pool3-selected element (B x flat)
+  float* hslab;            // fused fc head: fc1 split-K partials (ks x B x 128)
+  float* bn3part;          // fused fc head: BN3 backward sums per row group [2][32][nrg]
   float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
   double* ft2;             //   and the beta' bias terms [ci][co]
   float* slab;
@@ -3233,6 +3238,27 @@ int64_t c1w_blocks() {
     n = env_int("ABD_C1W_CAP", 0) > 0 ? env_int("ABD_C1W_CAP", 0) : (int64_t)cu * std::max(1, per);
   }
   return n;
+}
+
+// fused fc head launch geometry (fc_head.inc): head_fwd row tiles x position splits sized for about
+// one block per CU, head_mid row groups of 16
+struct HeadPlan {
+  int rt, ks, pp, nrg;
+};
+HeadPlan head_plan(const Geo& g, int64_t B) {
+  HeadPlan h;
+  h.rt = (int)((B + 31) / 32);
+  const int P = g.flat / 32;
+  const int want = std::max(1, std::min(P, (256 + h.rt - 1) / h.rt));
+  h.pp = std::min(kHeadPP, (P + want - 1) / want);
+  h.ks = (P + h.pp - 1) / h.pp;
+  h.nrg = (int)((B + kHeadRows - 1) / kHeadRows);
+  return h;
+}
+// the train step runs the fused fc head (ABD_FC_HEAD=0 restores the round-2 launches)
+bool head_on() {
+  static const bool on = env_int("ABD_FC_HEAD", 1) != 0;
+  return on;
 }
 
 Work layout(const abd_cnn* net, int64_t B, char* base) {
@@ -3284,6 +3310,12 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   w.partb2 = F(4096LL * 64);
   w.w2fold = F(64 * 256);     // BN1 fold: conv2 weights times alpha, bias terms (double)
   w.ft2 = reinterpret_cast<double*>(take(64 * 64 * sizeof(double)));
+  {
+    const HeadPlan hp = head_plan(g, B);
+    w.xh3 = F(B * g.flat);
+    w.hslab = F((int64_t)hp.ks * B * 128);
+    w.bn3part = F(2LL * 32 * hp.nrg);
+  }
   w.bytes = off;
   return w;
 }
@@ -3334,6 +3366,87 @@ PoolArgs pool_args(const Geo& g, int layer, int64_t B) {
 // extended window grid of bn_bwd_apply_kernel (windows tile the input: kernel == stride)
 int win_ext_h(const PoolArgs& a) { return std::max(a.Ho, (a.H + a.ph + a.sh - 1) / a.sh); }
 int win_ext_w(const PoolArgs& a) { return std::max(a.Wo, (a.W + a.pw + a.sw - 1) / a.sw); }
+
+// ---- fused fc head (fc_head.inc): arguments and the three launches
+HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* grads, int64_t B,
+                   const DropArgs& d1, const DropArgs& d2, const int64_t* labels, const int64_t* ind, float inv_batch,
+                   float* logprobs_out, int64_t* metrics, double loss_w) {
+  const Geo& g = net->g;
+  const HeadPlan hp = head_plan(g, B);
+  HeadArgs a{};
+  a.B = (int)B;
+  a.F = g.flat;
+  a.P = g.flat / 32;
+  a.K = g.K;
+  a.ks = hp.ks;
+  a.pp = hp.pp;
+  a.nrg = hp.nrg;
+  a.pool = pool_args(g, 3, B);
+  a.pool.r = w.r3;
+  a.pool.coef = w.coef + 128;
+  a.pool.dp = w.dp3;
+  a.drop1 = d1;
+  a.drop1.mask_out = w.mask1;
+  a.drop2 = d2;
+  a.drop2.mask_out = w.mask2;
+  a.f1t = w.f1t;
+  a.w1 = P.p[P_F1W];
+  a.b1 = P.p[P_F1B];
+  a.w2 = P.p[P_F2W];
+  a.b2 = P.p[P_F2B];
+  a.bn3w = P.p[P_BN3W];
+  a.labels = labels;
+  a.ind = ind;
+  a.inv_batch = inv_batch;
+  a.p3d = w.p3d;
+  a.xh3 = w.xh3;
+  a.slab = w.hslab;
+  a.d2 = w.d2;
+  a.logp = logprobs_out ? logprobs_out : w.logp;
+  a.dz = w.dz;
+  a.rowinfo = w.rowinfo;
+  a.da = w.da;
+  a.dp3 = w.dp3;
+  a.mask1 = w.mask1;
+  a.bn3part = w.bn3part;
+  float* G[P_COUNT];
+  for (int i = 0; i < P_COUNT; ++i) G[i] = grads ? grads + net->off[i] : nullptr;
+  a.g_f1w = G[P_F1W];
+  a.g_f1b = G[P_F1B];
+  a.g_f2w = G[P_F2W];
+  a.g_f2b = G[P_F2B];
+  a.g_bn3w = G[P_BN3W];
+  a.g_bn3b = G[P_BN3B];
+  a.metrics = metrics;
+  a.loss_w = loss_w;
+  a.dz3 = w.dz3;
+  a.partb3 = w.partb3;
+  a.hx = win_ext_h(a.pool);
+  a.wx = win_ext_w(a.pool);
+  a.n_w1 = 4 * ((g.flat + 31) / 32);
+  a.n_w2 = (g.K * 129 + 128 + kHeadW2 - 1) / kHeadW2;
+  a.n_apply = grid_for(B * a.hx * a.wx * 32 / 4, 2048);
+  return a;
+}
+
+// launch 1 (forward: pool3 + dropout1 + fc1 partials) / 2 (row head + dp3) / 3 (gradients + BN3 apply)
+int launch_head(int which, const HeadArgs& a, hipStream_t s) {
+  if (which == 1) {
+    abd::prof_begin(abd::PH_HEAD_FWD, s);
+    head_fwd_kernel<<<dim3((unsigned)((a.B + 31) / 32), (unsigned)a.ks), kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_HEAD_FWD, s);
+  } else if (which == 2) {
+    abd::prof_begin(abd::PH_HEAD_MID, s);
+    head_mid_kernel<<<dim3((unsigned)a.nrg, 8), kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_HEAD_MID, s);
+  } else {
+    abd::prof_begin(abd::PH_HEAD_BWD, s);
+    head_bwd_kernel<<<(unsigned)(a.n_w1 + a.n_w2 + 1 + a.n_apply), kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_HEAD_BWD, s);
+  }
+  ABD_LAUNCH_CHECK();
+  return 0;
+}
 
 NTArgs conv_fwd_args(const float* src, int Hs, int Ws, int Cs, int Ho, int Wo, int64_t B, const float* Bw, int N,
                      const float* bias, float* out) {
@@ -3800,7 +3913,7 @@ int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, co
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
             int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{},
-            const PrepArgs* prep = nullptr, bool fold1 = false) {
+            const PrepArgs* prep = nullptr, bool fold1 = false, const HeadArgs* head = nullptr) {
   // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
   // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
@@ -3935,6 +4048,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     } else
       bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN3W], P.p[P_BN3B], rm[2], rv[2], 32, w.coef + 128);
     ABD_LAUNCH_CHECK();
+    if (head) return launch_head(1, *head, s);  // BN3 + pool3 + dropout1 + fc1 partials (fc_head.inc)
     PoolArgs pa = pool_args(g, 3, B);
     pa.r = w.r3;
     pa.coef = inst ? inst_coef + B * 128 : w.coef + 128;
@@ -4061,8 +4175,10 @@ int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, d
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
-             int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0) {
+             int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0, const HeadArgs* head = nullptr) {
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
+  // head: the fused fc head ran its forward and row launches (fc_head.inc); its third launch -- fc
+  // gradients, counters, BN3 backward -- replaces everything down to conv3's weight gradient
   const hipStream_t sw = wgrad_stream(net, s);
   // SyncBN steps take the activation passes: the derived sums' small-gamma fallback (below) is decided
   // on the device, where the host-issued all-reduce of a second set of sums cannot follow it
@@ -4074,6 +4190,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
   const float s2 = 1.0f / (1.0f - kP2);
+  if (head) {
+    if (launch_head(3, *head, s)) return -1;
+    // fc1/fc2 gradients are final here (see below)
+    if (fc_grads_event) ABD_HIP(hipEventRecord(static_cast<hipEvent_t>(fc_grads_event), s));
+  } else {
   // ---- fc2 + dropout2/relu
   abd::prof_begin(abd::PH_FC2_BWD, s);
   {
@@ -4153,6 +4274,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
         return -1;
     }
   }
+  }  // !head
   // ---- pool3 / BN3 / relu backward -> dz3; conv3 wgrad + dgrad
   {
     PoolArgs pa = pool_args(g, 3, B);
@@ -4160,6 +4282,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.coef = w.coef + 128;
     pa.dp = w.dp3;
     pa.part = w.part;
+    if (head) {  // dz3 and the conv3 bias partials came from head_bwd_kernel
+      pa.nblk = head->n_apply;
+    } else {
     if (bn3_parts > 0) {  // partials from the fc1 data-gradient epilogue
       pa.nblk = bn3_parts;
     } else {
@@ -4181,6 +4306,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
+    }  // !head
     if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw3 = env_int("ABD_WGRAD_TR", 1) != 0;
@@ -4445,14 +4571,26 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   const bool fold1 = bn1_fold_ok(net, g, B) && !bn_sync_of(a).on();  // the fold rides on the single-rank finalize
   DropArgs d1 = make_drop(a, 1, w.mask1, g.flat), d2 = make_drop(a, 2, w.mask2, 128);
   const BnSync sy = bn_sync_of(a);
-  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep,
-              fold1))
-    return -1;
   const float inv = (a->grad_scale > 0.0f ? a->grad_scale : 1.0f) / (float)B;
-  // the metrics reduction rides on backward()'s fc2 gradient launch
-  if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
   const double loss_w = a->grad_scale > 0.0f ? (double)a->grad_scale : 1.0;
-  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w)) return -1;
+  // fused fc head (3 launches); SyncBN steps keep the round-2 launches (BN3's sums are all-reduced
+  // between the loss and the BN3 backward)
+  const bool use_head = head_on() && !sy.on();
+  HeadArgs ha{};
+  if (use_head)
+    ha = head_args(net, w, P, a->grads, B, d1, d2, a->labels, a->indicators, inv, a->logprobs_out, a->metrics, loss_w);
+  if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep,
+              fold1, use_head ? &ha : nullptr))
+    return -1;
+  if (use_head) {
+    if (launch_head(2, ha, s)) return -1;
+  } else {
+    // the metrics reduction rides on backward()'s fc2 gradient launch
+    if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
+  }
+  if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w,
+               use_head ? &ha : nullptr))
+    return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
