@@ -4433,7 +4433,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
            bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
                          P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s)))
         return -1;
-      if (!fold1) {  // the folded derivation has no division by gamma; otherwise guard it
+      {
+        // guard: (p - beta) / gamma unfolded; folded, the derivation is division-free but routes dy to
+        // the window's max / min r, while pool1 picks the first maximum of fl(alpha r + beta') -- the
+        // same element unless alpha is so small that the rounded values tie (at gamma = 0 every
+        // window ties and the reference routes to its first element)
         C1Args c1g = c1;
         c1g.nblk = (int)std::min<int64_t>(c1.nblk, kGuardBlocks);
         conv1_bwd_stats_guard_kernel<<<c1g.nblk, kT, 0, s>>>(c1g, P.p[P_BN1W], P.p[P_BN1B]);

@@ -51,6 +51,12 @@ def algorithmic_work(phase, B, H0, W0, K, n_mels, T, C, L):
         "fc1_fwd": 2.0 * B * 128 * flat,
         "fc1_wgrad": 2.0 * B * 128 * flat,
         "fc1_dgrad": 2.0 * B * 128 * flat,
+        # fused fc head (fc_head.inc), priced on its dense GEMM (fp32 MFMA): head_fwd = fc1 forward
+        # (+ pool3 / BN3 / dropout1), head_mid = fc1 data gradient (+ the per-row fc2 / loss head),
+        # head_bwd = fc1 weight gradient (+ fc2 gradients and BN3's backward apply)
+        "head_fwd": 2.0 * B * 128 * flat,
+        "head_mid": 2.0 * B * 128 * flat,
+        "head_bwd": 2.0 * B * 128 * flat,
     }
     if phase in fl:
         return fl[phase] / 1e12, "TFLOP/s", "mfma"
