@@ -12,7 +12,6 @@ running statistics are packed the same way.  The C ABI then sees plain pointers.
 from __future__ import annotations
 
 import ctypes as C
-import itertools
 
 import torch
 import torch.nn as nn
@@ -88,19 +87,22 @@ class _Engine:
             pass
 
 
-_MODEL_NONCE = itertools.count()
+def draw_dropout_nonce(device) -> int:
+    """One value drawn from the device's default generator when a model first binds to the device
+    (smallcnn.engine): models bound one after another -- flowmur.pretrain_model's surrogates, a
+    re-created model -- get their own dropout mask streams, as the reference's nn.Dropout draws from
+    the advancing device generator; torch.manual_seed / fix_random() before a model makes its draw,
+    and so its masks, reproducible (data-parallel ranks seeded alike agree on it)."""
+    return int(torch.randint(0, 1 << 62, (1,), device=device, dtype=torch.int64).item())
 
 
 def dropout_seed(device, model=None) -> int:
     """Seed of the device dropout hash: the device's default torch generator seed (set by
-    torch.manual_seed / fix_random(), utils/random_tools.py:5-18), mixed with the model's
-    creation nonce.  Nothing is drawn from the global CPU generator, as on the reference's CUDA
-    path where nn.Dropout consumes the device generator and the CPU stream only feeds the
+    torch.manual_seed / fix_random(), utils/random_tools.py:5-18) mixed with the model's nonce
+    (draw_dropout_nonce).  Nothing is drawn from the global CPU generator, as on the reference's
+    CUDA path where nn.Dropout consumes the device generator and the CPU stream only feeds the
     DataLoader shuffles -- so the batch order of every epoch matches the reference's under the
-    same seed.  The nonce (0 for the process's first smallcnn, which keeps the plain seed) gives
-    models built one after another -- flowmur.pretrain_model's surrogates, a re-created model --
-    their own mask streams, as the reference's advancing device generator does; data-parallel
-    ranks build their models in the same order, so they agree on it."""
+    same seed."""
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     base = int(torch.cuda.default_generators[idx].initial_seed())
@@ -143,7 +145,7 @@ class smallcnn(nn.Module):
         self.softmax = nn.Softmax(dim=1)
         self._engine = None
         self._step = 0
-        self._dropout_nonce = next(_MODEL_NONCE)
+        self._dropout_nonce = None   # drawn at the first bind to the device (draw_dropout_nonce)
         self.gemm_precision = "f32"   # "bf16": conv GEMMs on bf16 MFMA (set_gemm_precision)
         self.dropout_source = "device"  # "torch_cpu": the reference CPU path's exact masks
 
@@ -167,7 +169,8 @@ class smallcnn(nn.Module):
         # also the target of reference-format checkpoints (training.ReferencePickle), whose state is
         # a plain reference smallcnn's __dict__: fill in what this class adds
         super().__setstate__(state)
-        for k, v in (("_engine", None), ("_step", 0), ("gemm_precision", "f32"), ("dropout_source", "device")):
+        for k, v in (("_engine", None), ("_step", 0), ("gemm_precision", "f32"), ("dropout_source", "device"),
+                     ("_dropout_nonce", None)):
             if k not in self.__dict__:
                 self.__dict__[k] = v
 
@@ -219,6 +222,8 @@ class smallcnn(nn.Module):
         if eng is not None and (eng.H0, eng.W0) == (H0, W0) and eng.device == x.device and self._bound(eng):
             return eng
         new = _Engine(self, H0, W0, x.device)
+        if getattr(self, "_dropout_nonce", None) is None:
+            self._dropout_nonce = draw_dropout_nonce(x.device)
         with torch.no_grad():
             for p, v, name in zip(self._param_list(), new.views(new.params), PARAM_ORDER):
                 v.copy_(p.data.reshape(-1))
