@@ -24,7 +24,8 @@ EXPORTS = (
     "abd_mfcc_workspace_bytes", "abd_mfcc_f32", "abd_inject_waveform_f32", "abd_inject_workspace_bytes",
     "abd_pydub_overlay_i16", "abd_mfcc_deploy_backward_workspace_bytes", "abd_mfcc_deploy_backward",
     "abd_smallcnn_create", "abd_smallcnn_destroy", "abd_smallcnn_param_count", "abd_smallcnn_param_offsets",
-    "abd_smallcnn_flat_features", "abd_smallcnn_workspace_bytes", "abd_smallcnn_workspace_offset", "abd_smallcnn_bn1_folded", "abd_smallcnn_train_step",
+    "abd_smallcnn_flat_features", "abd_smallcnn_workspace_bytes", "abd_smallcnn_workspace_offset", "abd_smallcnn_bn1_folded", "abd_smallcnn_conv2_planes",
+    "abd_smallcnn_train_step",
     "abd_smallcnn_apply", "abd_smallcnn_forward", "abd_smallcnn_backward", "abd_smallcnn_eval", "abd_adam_f32",
     "abd_smallcnn_input_grad_workspace_bytes", "abd_smallcnn_input_grad",
     "abd_profile_start", "abd_profile_stop",
@@ -128,6 +129,7 @@ def _declare(lib):
         "abd_smallcnn_workspace_bytes": (sz, [vp, i64]),
         "abd_smallcnn_workspace_offset": (i64, [vp, i64, C.c_char_p]),
         "abd_smallcnn_bn1_folded": (C.c_int, [vp, i64]),
+        "abd_smallcnn_conv2_planes": (C.c_int, [vp, i64]),
         "abd_smallcnn_train_step": (i32, [vp, C.POINTER(TrainArgs), vp, sz, vp]),
         "abd_smallcnn_apply": (i32, [vp, C.POINTER(TrainArgs), vp, sz, vp]),
         "abd_smallcnn_forward": (i32, [vp, C.POINTER(TrainArgs), i32, vp, sz, vp]),

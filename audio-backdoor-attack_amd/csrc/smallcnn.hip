@@ -19,10 +19,36 @@
 #include "prof.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <vector>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Activations kept as exact bf16 planes (plane-major): np = 3 splits x = x0 + x1 + x2 exactly
+// (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1), np = 1 stores rne(x).  The conv2 GEMMs read
+// them as MFMA operands directly -- the split is done once, by the producer, instead of at every
+// use (4 taps x every tile) inside the GEMMs.  4 consecutive channels of element e -> one 8-B
+// store per plane.
+__device__ __forceinline__ void store_planes4(uint16_t* base, int64_t plane, int64_t e, float4 x, int np) {
+  f32x2 v[2] = {f32x2{x.x, x.y}, f32x2{x.z, x.w}};
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    if (pl >= np) break;
+    uint32_t u[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v[h], bf16x2));
+      const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+      v[h] -= back;  // exact: x - rne(x) fits in fp32
+    }
+    *reinterpret_cast<uint2*>(base + pl * plane + e) = make_uint2(u[0], u[1]);
+  }
+}
 
 namespace {
 
@@ -222,6 +248,11 @@ struct C1Args {
   PrepArgs prep;     // conv1_stats_kernel: blocks [0, nprep) repack the weights
   int nprep;
   const float* gamma;  // conv1_stats_fold_kernel: BN1 weight (the sign picks max or min per window)
+  // conv1_stats_fold_kernel: p1s != nullptr stores m as np exact bf16 planes (plane-major, plane
+  // stride `plane` elements; split once here instead of at every use in conv2's GEMMs) instead of p1
+  uint16_t* p1s;
+  int64_t plane;
+  int np;
 };
 
 // Stage x rows [h0, h0+kR1] of utterance b into LDS.
@@ -447,8 +478,9 @@ __global__ void __launch_bounds__(kT) conv1_stats_fold_kernel(C1Args a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           o[q] = neg[q] ? fminf(fminf(rr[0][q], rr[1][q]), rr[2][q]) : fmaxf(fmaxf(rr[0][q], rr[1][q]), rr[2][q]);
-        *reinterpret_cast<float4*>(a.p1 + (((int64_t)b * a.g.H1 + h0 + hl) * NWp + wo) * 64 + c0) =
-            make_float4(o[0], o[1], o[2], o[3]);
+        const int64_t e = (((int64_t)b * a.g.H1 + h0 + hl) * NWp + wo) * 64 + c0;
+        if (a.p1s != nullptr) store_planes4(a.p1s, a.plane, e, make_float4(o[0], o[1], o[2], o[3]), a.np);
+        else *reinterpret_cast<float4*>(a.p1 + e) = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
     __syncthreads();  // xs is restaged by the next chunk
@@ -1163,6 +1195,10 @@ struct PoolArgs {
   float* dz;           // NHWC
   float* part;
   int nblk;
+  // bn_bwd_apply_kernel: dzs != nullptr stores dz as dznp exact bf16 planes (plane stride dzplane)
+  uint16_t* dzs;
+  int64_t dzplane;
+  int dznp;
 };
 
 // Pool windows tile the grid (kernel == stride for both pools), so the pool kernels run one
@@ -1355,7 +1391,9 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a, int Hx, in
         f4set(dz, q, z);
         v[0][q] += z;
       }
-      *reinterpret_cast<float4*>(a.dz + ((wi.b * a.H + h) * a.W + w) * a.C + c0) = dz;
+      const int64_t e = ((int64_t)(wi.b * a.H + h) * a.W + w) * a.C + c0;
+      if (a.dzs != nullptr) store_planes4(a.dzs, a.dzplane, e, dz, a.dznp);
+      else *reinterpret_cast<float4*>(a.dz + e) = dz;
     }
   }
   cgroup_partials<1>(v, a.C, a.part, a.nblk, blockIdx.x);
@@ -1392,6 +1430,10 @@ struct NTArgs {
   const float* bnp;
   const float* bn_gamma;
   int bn_period;
+  // conv_ws_split_kernel<..., PA = true>: the A source as NP exact bf16 planes (plane-major, plane
+  // stride splane elements, same NHWC indexing as src)
+  const uint16_t* srcs;
+  int64_t splane;
 };
 
 constexpr int kBM = 128, kKC = 32;
@@ -1616,10 +1658,6 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
 // Tile: 128 rows x NB columns, K chunks of KB channels of one tap; LDS rows of KB + 8 bf16
 // (KB = 64: 144-B rows, so every 16-lane group of a ds_read_b128 hits 16 distinct 4-bank
 // groups); wave w owns rows 32w..32w+31 x all NB columns (NB / 32 accumulators).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // NP = 3 (ABD_PREC_F32_SPLIT): each fp32 operand x is staged as three bf16 planes x0 + x1 + x2 == x
 // exactly (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1: 8 + 8 + 8 significand bits), and the
@@ -1882,7 +1920,9 @@ template <> struct Terms<1> {
 // WPB = waves per block, NP = bf16 planes per operand (3: f32split, 1: bf16).  conv2: <2, 64, 2>
 // (101 KB of weights, one 8-wave block per CU); conv3 forward <1, 64, 1> and data gradient
 // <2, 32, 1> (48 KB, smaller tiles for their 150-180 k rows).
-template <int EPI, int NJ, int CS, int MI, int PDW, int WPB, int NP = 3>
+// PA: the A source comes pre-split (NTArgs::srcs, store_planes4): NP 16-B plane loads per fragment
+// replace the two fp32 loads and the in-register split.
+template <int EPI, int NJ, int CS, int MI, int PDW, int WPB, int NP = 3, bool PA = false>
 __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   constexpr int N = 32 * NJ, K = 4 * CS, LD = K + 8, KS = K / 16, TR = 32 * MI;
   static_assert(KS % PDW == 0, "a tile's K steps must be a whole number of ring turns");
@@ -1919,9 +1959,15 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   const int64_t g = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (SGPR)
   const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
   const int HoWo = a.Ho * a.Wo;
-  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)a.Hs * a.Ws * CS * 4 * (a.M / HoWo), 0x7ffffff0),
-      0x00020000);
+  constexpr uint32_t EB = PA ? 2u : 4u;  // bytes per source element
+  const __amdgpu_buffer_rsrc_t arsrc =
+      PA ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.srcs), 0,
+                                             (int)std::min<int64_t>((int64_t)NP * a.splane * 2, 0x7ffffff0), 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.src), 0,
+                                             (int)std::min<int64_t>((int64_t)a.Hs * a.Ws * CS * 4 * (a.M / HoWo),
+                                                                    0x7ffffff0),
+                                             0x00020000);
+  const uint32_t pstride = PA ? (uint32_t)(a.splane * 2) : 0u;  // bytes between planes
   constexpr uint32_t kOOB = 0x80000000u;
   const int kq = 8 * (lane >> 5);  // this lane's 8 channels / k inside a 16-deep step
   float st[NJ][2];
@@ -1948,7 +1994,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
       const int mm = ok ? m : r_lo;
       const int b = mm / HoWo, rem = mm - b * HoWo;
       const int h = rem / a.Wo, w = rem - h * a.Wo;
-      r.roff[i] = (uint32_t)((((int64_t)b * a.Hs + h) * a.Ws + w) * CS + kq) * 4u;
+      r.roff[i] = (uint32_t)((((int64_t)b * a.Hs + h) * a.Ws + w) * CS + kq) * EB;
       uint32_t mk = 0;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1964,15 +2010,18 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
       a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
   if (ntiles > 0) {
-    float4 raw[PDW][MI][2];  // [slot][i][lo/hi]: slot ks % PDW, refilled with the step PDW later once split
-    auto load = [&](const RowInfo& li, int ks, float4 (&r)[MI][2]) {
+    constexpr int NR = PA ? NP : 2;  // 16-B registers per A fragment: fp32 lo/hi, or the planes
+    uint4 raw[PDW][MI][NR];  // [slot][i][.]: slot ks % PDW, refilled with the step PDW later once used
+    auto load = [&](const RowInfo& li, int ks, uint4 (&r)[MI][NR]) {
       const int t = ks / (CS / 16), c16 = ks % (CS / 16);
-      const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * CS + c16 * 16) * 4);
+      const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * CS + c16 * 16) * EB);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const uint32_t off = ((li.tm[i] >> t) & 1u) ? li.roff[i] + tofs : kOOB;
-        r[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
-        r[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+          r[i][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  arsrc, (int)(off + (PA ? q * pstride : 16u * q)), 0, 0));
       }
     };
     f32x16 acc[MI][NJ];
@@ -1987,11 +2036,18 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
         for (int q = 0; q < NP; ++q)
           bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
     };
-    auto step = [&](int ks, float4 (&r)[MI][2], const RowInfo& li, int lks) {
+    auto step = [&](int ks, uint4 (&r)[MI][NR], const RowInfo& li, int lks) {
       bf16x8 av[MI][NP];
       bf16x8 (&bv)[NJ][NP] = bvs[ks & 1];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) planes_x8<NP>(r[i][0], r[i][1], av[i]);
+      for (int i = 0; i < MI; ++i) {
+        if constexpr (PA) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) av[i][q] = __builtin_bit_cast(bf16x8, r[i][PA ? q : 0]);
+        } else {
+          planes_x8<NP>(__builtin_bit_cast(float4, r[i][0]), __builtin_bit_cast(float4, r[i][NR - 1]), av[i]);
+        }
+      }
       // keep the refill behind the split: hoisted above it, the loads need fresh registers and
       // the loop-carried slot turns into copies that wait for the loads (a synchronous prefetch)
       __builtin_amdgcn_sched_barrier(0);
@@ -2367,6 +2423,10 @@ struct WGArgs {
   int R, cpb, nchunks, per;
   int dsz, bsz;      // LDS floats: dz part (16-B aligned) and one whole buffer
   float* slab;       // [gridDim.x][NB][4*CIN]
+  // conv_wgrad_trp_kernel<..., PS = true>: dz and src as NP exact bf16 planes (plane-major)
+  const uint16_t* dzs;
+  const uint16_t* srcs;
+  int64_t dzplane, srcplane;
 };
 
 // n16 16-byte pieces from g to l, lane-linear: wave-instruction j of wave w copies pieces
@@ -2733,9 +2793,16 @@ __global__ void __launch_bounds__(kT, NBUF == 1 ? 3 : 2) conv_wgrad_tr_kernel(WG
 #endif
 // NP = 1 (ABD_PREC_BF16): one RNE-rounded bf16 plane per operand and one MFMA term (a0 b0); the
 // staging of chunk c + 1 then rides on each step's single term.
-template <int R, int NB, int NS, int MAXS, int NP = 3>
+// PS: dz and src come pre-split (WGArgs::dzs / srcs, store_planes4): a slot loads its 4 channels'
+// NP planes (8 B each) and stores them as they are -- no split in the staging.
+template <int NP> struct PlaneSlot {
+  uint2 v[NP];
+};
+template <int R, int NB, int NS, int MAXS, int NP = 3, bool PS = false>
 __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
   constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4, Qd = 16 * NS;
+  constexpr uint32_t EB = PS ? 2u : 4u;  // bytes per staged element
+  using SlotT = typename std::conditional<PS, PlaneSlot<NP>, float4>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int Ws = a.Ws, Wo = a.Wo;
@@ -2754,13 +2821,13 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
       const int q = i / D4, r = q / Ws, w = q - r * Ws;
       c4 = i % D4;
       row = q;
-      off0[k] = (r < R && w < Wo) ? (uint32_t)(((r * Wo + w) * NB + 4 * c4) * 4) : kOOB;
+      off0[k] = (r < R && w < Wo) ? (uint32_t)(((r * Wo + w) * NB + 4 * c4) * EB) : kOOB;
     } else {
       const int q = (i - nd4) >> 4;
       c4 = (i - nd4) & 15;
       const bool ok = i < nd4 + ns4;
       row = ok ? Qd + q : Qd + Qs;  // trash row
-      off0[k] = (ok && q < (R + 1) * Ws) ? (uint32_t)((q * CIN + 4 * c4) * 4) : kOOB;
+      off0[k] = (ok && q < (R + 1) * Ws) ? (uint32_t)((q * CIN + 4 * c4) * EB) : kOOB;
     }
     loff[k] = (uint32_t)(row * kTrRow + c4 * 8);
   }
@@ -2772,13 +2839,33 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
-  auto fetch = [&](int c, float4 (&st)[MAXS]) {
+  auto fetch = [&](int c, SlotT (&st)[MAXS]) {
     const int b = c / a.cpb, h0 = (c - b * a.cpb) * R;
+    const uint32_t hdz = (uint32_t)(h0 * Wo * NB * EB), hsr = (uint32_t)(h0 * Ws * CIN * EB);
+    if constexpr (PS) {
+      // one descriptor per plane and utterance: rows past the utterance read zeros
+      __amdgpu_buffer_rsrc_t rdz[NP], rsr[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        rdz[q] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dzs) + q * a.dzplane + (int64_t)b * a.Ho * Wo * NB,
+                                                   0, a.Ho * Wo * NB * 2, 0x00020000);
+        rsr[q] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.srcs) + q * a.srcplane +
+                                                       (int64_t)b * a.Hs * Ws * CIN,
+                                                   0, a.Hs * Ws * CIN * 2, 0x00020000);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) {
+        const uint32_t o = off0[k] == kOOB ? kOOB : off0[k] + (isdz[k] ? hdz : hsr);
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+          st[k].v[q] = __builtin_bit_cast(uint2, isdz[k] ? __builtin_amdgcn_raw_buffer_load_b64(rdz[q], (int)o, 0, 0)
+                                                         : __builtin_amdgcn_raw_buffer_load_b64(rsr[q], (int)o, 0, 0));
+      }
+    } else {
     const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.dz) + (int64_t)b * a.Ho * Wo * NB, 0, a.Ho * Wo * NB * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.src) + (int64_t)b * a.Hs * Ws * CIN, 0, a.Hs * Ws * CIN * 4, 0x00020000);
-    const uint32_t hdz = (uint32_t)(h0 * Wo * NB * 4), hsr = (uint32_t)(h0 * Ws * CIN * 4);
 #pragma unroll
     for (int k = 0; k < MAXS; ++k) {
       if constexpr (ABD_TRP_ABL & 4) {
@@ -2789,9 +2876,16 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
       st[k] = __builtin_bit_cast(float4, isdz[k] ? __builtin_amdgcn_raw_buffer_load_b128(rdz, (int)o, 0, 0)
                                                  : __builtin_amdgcn_raw_buffer_load_b128(rsr, (int)o, 0, 0));
     }
+    }
   };
-  auto put_slot = [&](int k, const float4& v, unsigned char* buf) {
+  auto put_slot = [&](int k, const SlotT& vv, unsigned char* buf) {
     if constexpr (ABD_TRP_ABL & 2) return;
+    if constexpr (PS) {
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) *reinterpret_cast<uint2*>(buf + loff[k] + pl * 128) = vv.v[pl];
+      return;
+    }
+    const float4& v = reinterpret_cast<const float4&>(vv);
     f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
 #pragma unroll
     for (int pl = 0; pl < NP; ++pl) {
@@ -2839,8 +2933,8 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
                                                             acc[i][j], 0, 0, 0);
   };
   // chunk c from `cur`; chunk c + 1's registers stP -> `nxt`; chunk c + 2 -> stF
-  auto body = [&](int c, const unsigned char* cur, unsigned char* nxt, const float4 (&stP)[MAXS],
-                  float4 (&stF)[MAXS]) {
+  auto body = [&](int c, const unsigned char* cur, unsigned char* nxt, const SlotT (&stP)[MAXS],
+                  SlotT (&stF)[MAXS]) {
     __syncthreads();  // chunk c's images complete; every wave is done with chunk c - 1 (= nxt)
     fetch(min(c + 2, c1 - 1), stF);
     Frags F[2];
@@ -2871,7 +2965,7 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  float4 stA[MAXS], stB[MAXS];
+  SlotT stA[MAXS], stB[MAXS];
   unsigned char* buf0 = lds_tr;
   unsigned char* buf1 = lds_tr + bufb;
   if (c0 < c1) {
@@ -3190,6 +3284,8 @@ struct Work {
   float* xh3;              // fused fc head: xhat of each pool3-selected element (B x flat)
   float* hslab;            // fused fc head: fc1 split-K partials (ks x B x 128)
   float* bn3part;          // fused fc head: BN3 backward sums per row group [2][32][nrg]
+  uint16_t* p1s;           // conv2 plane mode: pool1 output m as exact bf16 planes [3][n_p1]
+  uint16_t* dz2s;          // conv2 plane mode: BN2-backward output dz2 as planes [3][n_r2]
   float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
   double* ft2;             //   and the beta' bias terms [ci][co]
   float* slab;
@@ -3316,6 +3412,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
     w.hslab = F((int64_t)hp.ks * B * 128);
     w.bn3part = F(2LL * 32 * hp.nrg);
   }
+  w.p1s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_p1 * sizeof(uint16_t)));
+  w.dz2s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_r2 * sizeof(uint16_t)));
   w.bytes = off;
   return w;
 }
@@ -3553,15 +3651,35 @@ int launch_wgrad_tr_n(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 // conv_wgrad_trp_kernel<R, NB, NS, MAXS> launch; -1 when the geometry is not this instantiation's
-template <int R, int NB, int NS, int MAXS, int NP = 3>
-int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
-                       float* slab, int phase, hipStream_t s) {
-  if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
+// geometry check of conv_wgrad_trp_kernel<R, NB, NS, MAXS, ...> (also used to decide the plane mode)
+template <int R, int NB, int NS, int MAXS>
+bool trp_fits(int Ho, int Wo, int Hs, int Ws) {
+  if (Ws != Wo + 1 || Hs < Ho + 1) return false;
   const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
-  if (Qd != 16 * NS || (Qd * (NB / 4) + Qs * 16 + kT - 1) / kT > MAXS) return -1;
+  if (Qd != 16 * NS || (Qd * (NB / 4) + Qs * 16 + kT - 1) / kT > MAXS) return false;
+  return 2 * (size_t)(Qd + Qs + 1) * kTrRow <= 160 * 1024;
+}
+// pl: pre-split planes (dzs / srcs, plane strides) for the PS instantiation, else nullptr
+struct WgPlanes {
+  const uint16_t* dzs;
+  const uint16_t* srcs;
+  int64_t dzplane, srcplane;
+};
+template <int R, int NB, int NS, int MAXS, int NP = 3, bool PS = false>
+int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
+                       float* slab, int phase, hipStream_t s, const WgPlanes* pl = nullptr) {
+  if (!trp_fits<R, NB, NS, MAXS>(Ho, Wo, Hs, Ws)) return -1;
+  if (PS && pl == nullptr) return -1;
+  const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
   WGArgs a{};
   a.dz = dz;
   a.src = src;
+  if (PS) {
+    a.dzs = pl->dzs;
+    a.srcs = pl->srcs;
+    a.dzplane = pl->dzplane;
+    a.srcplane = pl->srcplane;
+  }
   a.Ho = Ho;
   a.Wo = Wo;
   a.Hs = Hs;
@@ -3572,7 +3690,7 @@ int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs
   a.slab = slab;
   const size_t lds = 2 * (size_t)(Qd + Qs + 1) * kTrRow;
   if (lds > 160 * 1024) return -1;
-  auto* kern = &conv_wgrad_trp_kernel<R, NB, NS, MAXS, NP>;
+  auto* kern = &conv_wgrad_trp_kernel<R, NB, NS, MAXS, NP, PS>;
   static size_t cached = 0;
   static int per_cu = 1, n_cu = 256;
   if (cached != lds) {
@@ -3595,6 +3713,21 @@ int launch_wgrad_trp_n(const float* dz, const float* src, int Ho, int Wo, int Hs
   return grid;
 }
 
+// conv2's pre-split weight gradient: the first trp instantiation launch_wgrad_tr<.., 64> would pick
+template <int R>
+bool trp_planes_fit(int Ho, int Wo, int Hs, int Ws) {
+  return trp_fits<6, 64, 5, 11>(Ho, Wo, Hs, Ws) || trp_fits<R, 64, 2, 5>(Ho, Wo, Hs, Ws) ||
+         trp_fits<R, 64, 3, 8>(Ho, Wo, Hs, Ws) || trp_fits<R, 64, 1, 4>(Ho, Wo, Hs, Ws);
+}
+template <int R, int NP>
+int launch_wgrad_tr_planes(int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs, float* slab, int phase,
+                           hipStream_t s, const WgPlanes& pl) {
+  int r = launch_wgrad_trp_n<6, 64, 5, 11, NP, true>(nullptr, nullptr, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s, &pl);
+  if (r < 0) r = launch_wgrad_trp_n<R, 64, 2, 5, NP, true>(nullptr, nullptr, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s, &pl);
+  if (r < 0) r = launch_wgrad_trp_n<R, 64, 3, 8, NP, true>(nullptr, nullptr, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s, &pl);
+  if (r < 0) r = launch_wgrad_trp_n<R, 64, 1, 4, NP, true>(nullptr, nullptr, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s, &pl);
+  return r;
+}
 template <int R, int NB, int NP = 3>
 int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                     float* slab, int phase, hipStream_t s) {
@@ -3720,15 +3853,17 @@ int ws_blocks(int N, int Cs) {
   static const int m3 = std::max(1, env_int("ABD_WS3_MULT", 1));
   return (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
 }
-template <int EPI, int NP = 3>
+template <int EPI, int NP = 3, bool PA = false>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
+  if (PA && (a.srcs == nullptr || a.N != 64 || a.Cs != 64)) return -1;
   const int nb = ws_blocks(a.N, a.Cs);
   if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
   if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
   static const int cfg = env_int("ABD_WS_CFG", 2);  // conv2 tile / ring / waves-per-block (A/B knob)
-  if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
+  if (PA) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
   else if (a.N == 64 && a.Cs == 64 && (cfg == 2 || NP == 1)) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
   else if (NP == 3 && a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
   else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
@@ -3913,7 +4048,9 @@ int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, co
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
             int64_t* nbt = nullptr, float4* inst_coef = nullptr, const BnSync& sy = BnSync{},
-            const PrepArgs* prep = nullptr, bool fold1 = false, const HeadArgs* head = nullptr) {
+            const PrepArgs* prep = nullptr, bool fold1 = false, const HeadArgs* head = nullptr, int planes = 0) {
+  // planes > 0: conv2 plane mode (conv2_planes): conv1_stats_fold_kernel writes m as planes, conv2
+  // reads them
   // inst_coef != nullptr: every utterance is its own BatchNorm batch (B x 160 float4 of
   // coefficients), running statistics untouched -- a batch of batch-1 train-mode forwards
   const Geo& g = net->g;
@@ -3955,6 +4092,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     abd::prof_begin(abd::PH_CONV1_STATS, s);
     if (fold1) {
       c1.gamma = P.p[P_BN1W];
+      if (planes > 0) {
+        c1.p1s = w.p1s;
+        c1.plane = B * g.H1 * g.W1p * 64;
+        c1.np = planes;
+      }
       c1.nblk = (int)std::min<int64_t>(c1.nblk, c1f_blocks());  // one resident round
       conv1_stats_fold_kernel<<<c1.nblk + c1.nprep, kT, 0, s>>>(c1);
     } else {
@@ -3994,7 +4136,13 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
       a.fold_t = w.ft2;
     }
     static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
-    if (ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
+    if (planes > 0) {
+      a.srcs = w.p1s;
+      a.splane = B * g.H1 * g.W1p * 64;
+    }
+    if (planes == 3 ? launch_conv_ws_split<EPI_CONV, 3, true>(a, s, abd::PH_CONV2_FWD)
+        : planes == 1 ? launch_conv_ws_split<EPI_CONV, 1, true>(a, s, abd::PH_CONV2_FWD)
+        : ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
                  : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD))
            : bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
            : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
@@ -4128,6 +4276,22 @@ bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
          split_mi() == 1 &&
          (int64_t)g.H1 * g.W1p * 64 * 4 * B < 0x7ffffff0LL;
 }
+// conv2 plane mode: the train step keeps conv2's two activation operands -- the pool1 output m (BN1
+// fold) and the BN2-backward output dz2 -- as exact bf16 planes written by their producers
+// (conv1_stats_fold_kernel, bn_bwd_apply_kernel), and conv2's forward, data- and weight-gradient
+// kernels read the planes as MFMA operands (no per-use split).  Returns the plane count (3 in
+// f32split, 1 in bf16) or 0 (fp32 buffers; ABD_PLANES=0 forces it).
+int conv2_planes(const abd_cnn* net, const Geo& g, int64_t B, bool fold1) {
+  static const bool on = env_int("ABD_PLANES", 1) != 0;
+  if (!on || !fold1) return 0;
+  const int np = net->precision == ABD_PREC_F32_SPLIT ? 3 : net->precision == ABD_PREC_BF16 ? 1 : 0;
+  if (np == 0 || !ws_on() || split_mi() != 1 || (np == 3 && env_int("ABD_WS_CFG", 2) != 2)) return 0;
+  const int64_t n_p1 = B * g.H1 * g.W1p * 64, n_r2 = B * g.H2 * g.W2 * 64;
+  if ((int64_t)3 * std::max(n_p1, n_r2) * 2 >= 0x7ffffff0LL) return 0;  // 32-bit buffer offsets
+  if (!trp_planes_fit<2>(g.H2, g.W2, g.H1, g.W1p)) return 0;
+  return np;
+}
+
 // Stream for the conv weight gradients: they depend only on dz and the stored forward activations and
 // feed nothing but the final gradient buffer, so they run on a side stream of the net while the data-
 // gradient chain (dgrad -> BN backward -> ...) continues on the caller's stream; backward() joins it
@@ -4175,7 +4339,8 @@ int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, d
 
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
-             int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0, const HeadArgs* head = nullptr) {
+             int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0, const HeadArgs* head = nullptr,
+             int planes = 0) {
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   // head: the fused fc head ran its forward and row launches (fc_head.inc); its third launch -- fc
   // gradients, counters, BN3 backward -- replaces everything down to conv3's weight gradient
@@ -4368,6 +4533,11 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     }
     pa.bcoef = w.bcoef + 64;
     pa.dz = w.dz2;
+    if (planes > 0) {  // conv2 plane mode: dz2 as planes for conv2's data and weight gradients
+      pa.dzs = w.dz2s;
+      pa.dzplane = B * g.H2 * g.W2 * 64;
+      pa.dznp = planes;
+    }
     pa.part = w.partb2;
     pa.nblk = grid_for(B * win_ext_h(pa) * win_ext_w(pa) * 64 / 4);
     abd::prof_begin(abd::PH_BN2_BWD, s);
@@ -4377,7 +4547,12 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (stream_dep(net->ev_fork, s, sw)) return -1;
     const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
     static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
-    int nsl = net->precision == ABD_PREC_BF16
+    const WgPlanes wpl{w.dz2s, w.p1s, B * g.H2 * g.W2 * 64, B * g.H1 * g.W1p * 64};
+    int nsl = planes == 3 ? launch_wgrad_tr_planes<2, 3>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                                         abd::PH_CONV2_WGRAD, sw, wpl)
+              : planes == 1 ? launch_wgrad_tr_planes<2, 1>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                                           abd::PH_CONV2_WGRAD, sw, wpl)
+              : net->precision == ABD_PREC_BF16
                   ? launch_wgrad_tr<2, 64, 1>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
                                               abd::PH_CONV2_WGRAD, sw)
               : (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
@@ -4387,6 +4562,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                          : launch_wgrad_tr<2, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
                                                   abd::PH_CONV2_WGRAD, sw))
                   : -1;
+    ABD_CHECK(planes == 0 || nsl >= 0, ABD_E_UNSUPPORTED, "conv2 plane-mode weight gradient geometry");
     if (nsl < 0)
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
                                       spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
@@ -4398,7 +4574,13 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
-    if ((net->precision == ABD_PREC_BF16
+    if (planes > 0) {
+      da.srcs = w.dz2s;
+      da.splane = B * g.H2 * g.W2 * 64;
+    }
+    if ((planes == 3 ? launch_conv_ws_split<EPI_STORE, 3, true>(da, s, abd::PH_CONV2_DGRAD)
+         : planes == 1 ? launch_conv_ws_split<EPI_STORE, 1, true>(da, s, abd::PH_CONV2_DGRAD)
+         : net->precision == ABD_PREC_BF16
              ? (launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV2_DGRAD) == 0
                     ? 0
                     : launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD))
@@ -4539,6 +4721,11 @@ int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch) {
   return (net && batch >= 1 && bn1_fold_ok(net, net->g, batch)) ? 1 : 0;
 }
 
+int abd_smallcnn_conv2_planes(const abd_cnn* net, int64_t batch) {
+  if (!net || batch < 1) return 0;
+  return conv2_planes(net, net->g, batch, bn1_fold_ok(net, net->g, batch));
+}
+
 int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name) {
   if (!net || !name) return -1;
   char* base = reinterpret_cast<char*>(static_cast<uintptr_t>(4096));  // any non-null base: offsets only
@@ -4549,7 +4736,8 @@ int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const c
   } tab[] = {{"p1", w.p1},     {"r2", w.r2},       {"p2", w.p2},     {"r3", w.r3},       {"p3d", w.p3d},
              {"d2", w.d2},     {"logp", w.logp},   {"dz", w.dz},     {"dp3", w.dp3},     {"da", w.da},
              {"dz3", w.dz3},   {"dp2", w.dp2},     {"dz2", w.dz2},   {"dp1", w.dp1},     {"coef", w.coef},
-             {"bcoef", w.bcoef}, {"mask1", w.mask1}, {"mask2", w.mask2}, {"rowinfo", w.rowinfo}};
+             {"bcoef", w.bcoef}, {"mask1", w.mask1}, {"mask2", w.mask2}, {"rowinfo", w.rowinfo},
+             {"p1s", w.p1s},   {"dz2s", w.dz2s},   {"xh3", w.xh3}};
   for (const auto& t : tab)
     if (strcmp(t.n, name) == 0) return (int64_t)(static_cast<const char*>(t.p) - base);
   return -1;
@@ -4583,8 +4771,9 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
   HeadArgs ha{};
   if (use_head)
     ha = head_args(net, w, P, a->grads, B, d1, d2, a->labels, a->indicators, inv, a->logprobs_out, a->metrics, loss_w);
+  const int planes = conv2_planes(net, g, B, fold1);
   if (forward(net, w, P, a->x, B, a->running, a->running, true, d1, d2, s, a->num_batches_tracked, nullptr, sy, &prep,
-              fold1, use_head ? &ha : nullptr))
+              fold1, use_head ? &ha : nullptr, planes))
     return -1;
   if (use_head) {
     if (launch_head(2, ha, s)) return -1;
@@ -4593,7 +4782,7 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
     if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
   }
   if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w,
-               use_head ? &ha : nullptr))
+               use_head ? &ha : nullptr, planes))
     return -1;
   copy_masks(a, w, g, B, s);
   if (a->do_update) {

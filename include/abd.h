@@ -229,13 +229,19 @@ int abd_smallcnn_param_offsets(const abd_cnn* net, int64_t* offsets /* 17 */);
 int abd_smallcnn_flat_features(const abd_cnn* net);
 size_t abd_smallcnn_workspace_bytes(const abd_cnn* net, int64_t batch);
 /* Byte offset of a named activation buffer inside the workspace (tests / debugging):
- * p1 r2 p2 r3 p3d d2 logp dz dp3 da dz3 dp2 dz2 dp1 coef bcoef mask1 mask2 rowinfo. */
+ * p1 r2 p2 r3 p3d d2 logp dz dp3 da dz3 dp2 dz2 dp1 coef bcoef mask1 mask2 rowinfo p1s dz2s xh3. */
 int64_t abd_smallcnn_workspace_offset(const abd_cnn* net, int64_t batch, const char* name);
 /* 1 when abd_smallcnn_train_step at this batch folds BN1 into conv2 (ABD_PREC_F32_SPLIT; a step
  * with SyncBN (abd_train_args.bn_sync set) never folds): the workspace's p1 then holds m, the
  * pool1-selected relu(conv1) value per window, and p1 = alpha * m + beta' with BN1's coefficients
  * (coef[0][c] = (mean, invstd, alpha, beta')); 0 otherwise. */
 int abd_smallcnn_bn1_folded(const abd_cnn* net, int64_t batch);
+/* Plane count of the conv2 plane mode of abd_smallcnn_train_step at this batch (no SyncBN): 3
+ * (ABD_PREC_F32_SPLIT) or 1 (ABD_PREC_BF16) when the step keeps conv2's two activation operands as
+ * exact bf16 planes -- the workspace's "p1s" (pool1 output m, [planes][B*H1*W1p*64] uint16, replacing
+ * p1) and "dz2s" (BN2 backward output, [planes][B*H2*W2*64], replacing dz2), x = sum of the planes
+ * exactly for 3 planes, rne(x) for 1 -- else 0 (p1 / dz2 hold fp32). */
+int abd_smallcnn_conv2_planes(const abd_cnn* net, int64_t batch);
 
 /* Device-side counters written by the train/eval launches (int64 / double):
  *   [0] sum of per-batch mean losses (double bits; train steps weight each by

@@ -28,6 +28,23 @@ def ws_array(eng, ws, B, name, shape, dtype=torch.float32):
     return ws[off:off + n].view(dtype).view(*shape).cpu().numpy()
 
 
+def planes_sum(eng, ws, B, name, shape, planes):
+    """A conv2 plane-mode buffer ("p1s" / "dz2s": `planes` exact bf16 planes, plane-major) as the
+    float64 value it represents (the sum of its planes; abd_smallcnn_conv2_planes)."""
+    n = int(np.prod(shape))
+    raw = ws_array(eng, ws, B, name, (planes, n), dtype=torch.int16).astype(np.uint16)
+    vals = (raw.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    return vals.sum(axis=0).reshape(shape)
+
+
+def ws_float(eng, ws, B, name, shape):
+    """p1 / dz2 whichever way the last train step stored them (fp32 buffer or conv2 planes)."""
+    planes = L.lib().abd_smallcnn_conv2_planes(eng.h, B)
+    if planes and name in ("p1", "dz2"):
+        return planes_sum(eng, ws, B, name + "s", shape, planes)
+    return ws_array(eng, ws, B, name, shape).astype(np.float64)
+
+
 def decisions(eng, B, x, params, geo, ws=None):
     """GPU decisions for the last forward kept in eng's workspace (or ``ws``)."""
     ws = eng.workspace(B) if ws is None else ws

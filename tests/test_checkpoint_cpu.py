@@ -67,19 +67,8 @@ def test_whole_module_checkpoint_round_trip(tmp_path):
     """Under the drop-in (abd_amd.run puts dropin/ first: flowmur.py:55 reloads its benign model),
     the pickle resolves utils.models.smallcnn to the accelerated class."""
     m, path = _write_checkpoint(tmp_path)
-    dropin = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                          "audio-backdoor-attack_amd", "dropin")
-    saved = {k: v for k, v in sys.modules.items() if k == "utils" or k.startswith("utils.")}
-    for k in saved:
-        del sys.modules[k]
-    sys.path.insert(0, dropin)
-    try:
-        loaded = torch.load(path, weights_only=False)   # written by this test
-    finally:
-        sys.path.remove(dropin)
-        for k in [k for k in sys.modules if k == "utils" or k.startswith("utils.")]:
-            del sys.modules[k]
-        sys.modules.update(saved)
+    from conftest import load_dropin_checkpoint
+    loaded = load_dropin_checkpoint(path)
     assert isinstance(loaded, smallcnn) and loaded._engine is None and loaded._step == 0
     assert loaded.gemm_precision == "f32" and not loaded.training
     a, b = m.state_dict(), loaded.state_dict()

@@ -15,6 +15,7 @@ import abd_amd
 from abd_amd import models as M, training as T, _lib as L
 from golden_inputs import make_state, mfcc_like
 from oracle import smallcnn as oc
+from gpu_replay import ws_float
 
 pytestmark = pytest.mark.gpu
 
@@ -67,13 +68,13 @@ def test_bf16_gemms_exact_on_rounded_operands(dev, shape, prec):
     T.train_step(m, x, y, torch.zeros(B, dtype=torch.int64, device=dev), None, None, seed=3)
     torch.cuda.synchronize()
     ws = eng.workspace(B)
-    p1 = ws_view(eng, ws, B, "p1", (B, g["H1p"], g["W1p"], 64))
+    p1 = ws_float(eng, ws, B, "p1", (B, g["H1p"], g["W1p"], 64))   # fp32 buffer or conv2 planes
     r2 = ws_view(eng, ws, B, "r2", (B, g["H2"], g["W2"], 64))
     p2 = ws_view(eng, ws, B, "p2", (B, g["H2p"], g["W2p"], 64))
     r3 = ws_view(eng, ws, B, "r3", (B, g["H3"], g["W3"], 32))
     dz3 = ws_view(eng, ws, B, "dz3", (B, g["H3"], g["W3"], 32))
     dp2 = ws_view(eng, ws, B, "dp2", (B, g["H2p"], g["W2p"], 64))
-    dz2 = ws_view(eng, ws, B, "dz2", (B, g["H2"], g["W2"], 64))
+    dz2 = ws_float(eng, ws, B, "dz2", (B, g["H2"], g["W2"], 64))
     dp1 = ws_view(eng, ws, B, "dp1", (B, g["H1p"], g["W1p"], 64))
     w2 = rnd(st["conv2.weight"])
     w3 = rnd(st["conv3.weight"])

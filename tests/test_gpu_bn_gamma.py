@@ -15,7 +15,7 @@ import torch
 import abd_amd
 from abd_amd import models as M, training as T
 from golden_inputs import make_state, mfcc_like
-from gpu_replay import decisions
+from gpu_replay import decisions, ws_float
 from oracle import smallcnn as oc
 from test_gpu_layers import ws_view, nrel
 
@@ -62,7 +62,7 @@ def test_tiny_gamma_gradients_match_oracle(prec):
     nhwc = lambda a: np.transpose(a, (0, 2, 3, 1))  # noqa: E731
     ws = eng.workspace(B)
     for name, shp in (("dz3", (B, g["H3"], g["W3"], 32)), ("dz2", (B, g["H2"], g["W2"], 64))):
-        report[name] = nrel(ws_view(eng, ws, B, name, shp), nhwc(rec[name]))
+        report[name] = nrel(ws_float(eng, ws, B, name, shp), nhwc(rec[name]))
     # the tiny channels' own BN gradients, elementwise against the layer's scale
     for i in (1, 2, 3):
         for n in (f"bn{i}.weight", f"bn{i}.bias"):

@@ -187,8 +187,8 @@ def test_eval_model_loop_through_dropins_and_checkpoint(dev, tmp_path):
     assert np.all(np.isfinite(h)) and h[-1, 0] < h[0, 0]
     assert res["n_poison"] == int(res["n_train"] * 0.1)
     # the early-stopping checkpoint loads in another process and runs
-    ck = torch.load(str(tmp_path / "record" / "badnets_smallcnn" / "checkpoint.pt"), map_location=dev,
-                    weights_only=False)
+    from conftest import load_dropin_checkpoint
+    ck = load_dropin_checkpoint(str(tmp_path / "record" / "badnets_smallcnn" / "checkpoint.pt"), map_location=dev)
     ck.eval()
     with torch.no_grad():
         y = ck(torch.zeros((2, 1, 101, 40), device=dev))

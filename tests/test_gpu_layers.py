@@ -9,7 +9,7 @@ import abd_amd
 from abd_amd import models as M, training as T, _lib as L
 from golden_inputs import make_state, mfcc_like, patch
 from oracle import smallcnn as oc
-from gpu_replay import decisions
+from gpu_replay import decisions, ws_float
 
 pytestmark = pytest.mark.gpu
 
@@ -83,7 +83,7 @@ def test_every_buffer_matches_oracle(shape, prec):
     coef1 = ws_view(eng, ws, B, "coef", (3, 64, 4))[0]
     report = {}
     for name, ref, tf, shp, tol in checks:
-        got = ws_view(eng, ws, B, name, shp)
+        got = ws_float(eng, ws, B, name, shp) if name in ("p1", "dz2") else ws_view(eng, ws, B, name, shp)
         if name == "p1" and folded:  # p1 = alpha * m + beta' (what conv2's folded weights / bias apply)
             got = got.astype(np.float64) * coef1[:, 2] + coef1[:, 3]
         refv = tf(ref) if tf else ref
