@@ -201,15 +201,18 @@ __device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
 }
 
 // weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets), fc1^T
+constexpr int kGuardTickets = 4;  // BN1, BN2 guard tickets (+ spares)
 struct PrepArgs {
   const float *c2w, *c3w, *f1w;
   int flat;
   float *w2f, *w2d, *w3f, *w3d, *f1t;
+  unsigned* tickets;  // the step's guard tickets (bn_guard_*_kernel), zeroed here every step
 };
 
 __device__ __forceinline__ void prep_weights_body(const PrepArgs& a, int bx, int nb) {
   const int64_t n2 = 64 * 64 * 4, n3 = 32 * 64 * 4, nf = 128LL * a.flat;
   const int64_t total = n2 + n3 + nf;
+  if (bx == 0 && threadIdx.x < kGuardTickets && a.tickets != nullptr) a.tickets[threadIdx.x] = 0u;
   for (int64_t e = bx * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)nb * kT) {
     if (e < n2) {
       const int co = (int)(e / 256), ci = (int)(e / 4 % 64), t = (int)(e % 4);
@@ -504,10 +507,67 @@ __device__ __forceinline__ bool bn_any_tiny(const float* __restrict__ gamma, con
 
 __device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a);
 __global__ void __launch_bounds__(kT) conv1_bwd_stats_kernel(C1Args a) { conv1_bwd_stats_body(a); }
+// The guarded fallbacks' finalize, in the same launch: every block publishes its partials, the last
+// block to arrive (agent-scope release -> ticket -> acquire, MI355X_MICROARCH.md inter-workgroup
+// visibility) reduces them per channel exactly as bn_bwd_finalize_kernel does and overwrites the
+// derived dgamma / dbeta / backward coefficients.  The ticket is zeroed by the step's prep blocks.
+struct GuardOut {
+  double count;
+  const float4* coef;
+  float* dgamma;
+  float* dbeta;
+  BCoef* bcoef;
+  unsigned* ticket;
+};
+__device__ __forceinline__ bool guard_last_block(unsigned* ticket) {
+  __shared__ unsigned last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1u : 0u;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  return last != 0u;
+}
+__device__ __forceinline__ void guard_finalize(const float* part, int nblk, int C, const float* gamma, const GuardOut& g) {
+  __shared__ double red[2][kT / kWave];
+  for (int c = 0; c < C; ++c) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += kT) {
+      s1 += part[(int64_t)c * nblk + i];
+      s2 += part[((int64_t)C + c) * nblk + i];
+    }
+    s1 = abd::wave_sum_d(s1);
+    s2 = abd::wave_sum_d(s2);
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = s1;
+      red[1][threadIdx.x >> 6] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s1 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      g.dgamma[c] = (float)s2;
+      g.dbeta[c] = (float)s1;
+      const double gg = (double)gamma[c] * (double)g.coef[c].y, mdy = s1 / g.count, mdyx = s2 / g.count;
+      const double mean = (double)g.coef[c].x, invstd = (double)g.coef[c].y;
+      g.bcoef[c] = BCoef{gg, gg * (mdyx * invstd * mean - mdy), -gg * mdyx * invstd, 0.0};
+    }
+    __syncthreads();
+  }
+}
+
 // guarded fallback: BN1's statistics from the activations when a gamma is tiny (bn_any_tiny)
-__global__ void __launch_bounds__(kT) conv1_bwd_stats_guard_kernel(C1Args a, const float* gamma, const float* beta) {
+__global__ void __launch_bounds__(kT) conv1_bwd_stats_guard_kernel(C1Args a, const float* gamma, const float* beta,
+                                                                   GuardOut go) {
   if (!bn_any_tiny(gamma, beta, 64)) return;
   conv1_bwd_stats_body(a);
+  if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, 64, gamma, go);
 }
 __device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
@@ -1320,9 +1380,10 @@ __device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a);
 __global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) { bn_pool_bwd_stats_body(a); }
 // guarded fallback: BN2 / BN3 statistics from the activations when a gamma is tiny (bn_any_tiny)
 __global__ void __launch_bounds__(kT) bn_pool_bwd_stats_guard_kernel(PoolArgs a, const float* gamma,
-                                                                     const float* beta) {
+                                                                     const float* beta, GuardOut go) {
   if (!bn_any_tiny(gamma, beta, a.C)) return;
   bn_pool_bwd_stats_body(a);
+  if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, a.C, gamma, go);
 }
 __device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a) {
   const int CG = a.C / 4;
@@ -3286,6 +3347,7 @@ struct Work {
   float* bn3part;          // fused fc head: BN3 backward sums per row group [2][32][nrg]
   uint16_t* p1s;           // conv2 plane mode: pool1 output m as exact bf16 planes [3][n_p1]
   uint16_t* dz2s;          // conv2 plane mode: BN2-backward output dz2 as planes [3][n_r2]
+  unsigned* tickets;       // guarded BN fallbacks' arrival tickets (zeroed by the prep blocks)
   float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
   double* ft2;             //   and the beta' bias terms [ci][co]
   float* slab;
@@ -3414,6 +3476,7 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   }
   w.p1s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_p1 * sizeof(uint16_t)));
   w.dz2s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_r2 * sizeof(uint16_t)));
+  w.tickets = reinterpret_cast<unsigned*>(take(kGuardTickets * sizeof(unsigned)));
   w.bytes = off;
   return w;
 }
@@ -3429,7 +3492,7 @@ Params params_of(const abd_cnn* net, const float* flat) {
 }
 
 PrepArgs prep_args(const Params& P, const Work& w, const Geo& g) {
-  return PrepArgs{P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t};
+  return PrepArgs{P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t, w.tickets};
 }
 unsigned prep_blocks(const Geo& g) { return (unsigned)grid_for(64 * 256 + 32 * 256 + 128LL * g.flat); }
 
@@ -3522,7 +3585,7 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.hx = win_ext_h(a.pool);
   a.wx = win_ext_w(a.pool);
   a.n_w1 = 4 * ((g.flat + 31) / 32);
-  a.n_w2 = (g.K * 129 + 128 + kHeadW2 - 1) / kHeadW2;
+  a.n_w2 = 4 * ((g.K + 31) / 32) + (g.K + 128 + kHeadW2 - 1) / kHeadW2;  // fc2 weight tiles + bias sums
   a.n_apply = grid_for(B * a.hx * a.wx * 32 / 4, 2048);
   return a;
 }
@@ -4280,11 +4343,15 @@ bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
 // fold) and the BN2-backward output dz2 -- as exact bf16 planes written by their producers
 // (conv1_stats_fold_kernel, bn_bwd_apply_kernel), and conv2's forward, data- and weight-gradient
 // kernels read the planes as MFMA operands (no per-use split).  Returns the plane count (3 in
-// f32split, 1 in bf16) or 0 (fp32 buffers; ABD_PLANES=0 forces it).
+// f32split, 1 in bf16) or 0 (fp32 buffers).  Measured (r3_v2, B = 512 ultrasonic): in f32split the
+// planes are 6 B per element against fp32's 4, and the weight-stationary GEMMs re-read every operand
+// row for 4 taps from L2 -- conv2 forward 0.144 -> 0.235 ms, data gradient 0.129 -> 0.184, weight
+// gradient 0.121 -> 0.152, BN2 backward +11 us: off by default there (ABD_PLANES=3 enables it).
+// bf16 (one 2-B plane) halves the operand bytes instead: on by default (ABD_PLANES=0 disables).
 int conv2_planes(const abd_cnn* net, const Geo& g, int64_t B, bool fold1) {
-  static const bool on = env_int("ABD_PLANES", 1) != 0;
-  if (!on || !fold1) return 0;
-  const int np = net->precision == ABD_PREC_F32_SPLIT ? 3 : net->precision == ABD_PREC_BF16 ? 1 : 0;
+  static const int mode = env_int("ABD_PLANES", 1);  // 0 off, 1 bf16 only, 3 bf16 and f32split
+  if (mode == 0 || !fold1) return 0;
+  const int np = (net->precision == ABD_PREC_F32_SPLIT && mode == 3) ? 3 : net->precision == ABD_PREC_BF16 ? 1 : 0;
   if (np == 0 || !ws_on() || split_mi() != 1 || (np == 3 && env_int("ABD_WS_CFG", 2) != 2)) return 0;
   const int64_t n_p1 = B * g.H1 * g.W1p * 64, n_r2 = B * g.H2 * g.W2 * 64;
   if ((int64_t)3 * std::max(n_p1, n_r2) * 2 >= 0x7ffffff0LL) return 0;  // 32-bit buffer offsets
@@ -4325,14 +4392,12 @@ int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
 // Guarded fallback of the derived BN2 / BN3 backward statistics (bn_any_tiny): the activation pass
 // and its finalize over at most kGuardBlocks blocks, both exiting at once unless a gamma is tiny;
 // they overwrite dgamma / dbeta / bcoef written by the derivation.  w.part is free at this point.
-constexpr int kGuardBlocks = 256;
+constexpr int kGuardBlocks = 64;
 int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, double count, const float4* coef,
-                 float* dgamma, float* dbeta, BCoef* bcoef, hipStream_t s) {
+                 float* dgamma, float* dbeta, BCoef* bcoef, unsigned* ticket, hipStream_t s) {
   PoolArgs pa = pa_in;
   pa.nblk = std::min(grid_for((int64_t)pa.B * pa.Ho * pa.Wo * pa.C / 4), kGuardBlocks);
-  bn_pool_bwd_stats_guard_kernel<<<pa.nblk, kT, 0, s>>>(pa, gamma, beta);
-  ABD_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<pa.C, kT, 0, s>>>(pa.part, pa.nblk, pa.C, count, gamma, coef, dgamma, dbeta, bcoef, beta);
+  bn_pool_bwd_stats_guard_kernel<<<pa.nblk, kT, 0, s>>>(pa, gamma, beta, GuardOut{count, coef, dgamma, dbeta, bcoef, ticket});
   ABD_LAUNCH_CHECK();
   return 0;
 }
@@ -4461,7 +4526,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                         G[P_BN3B], w.bcoef + 128, s))
       return -1;
     if (bn3_parts > 0 && bn_bwd_guard(pa, P.p[P_BN3W], P.p[P_BN3B], (double)B * g.H3 * g.W3, w.coef + 128, G[P_BN3W],
-                                      G[P_BN3B], w.bcoef + 128, s))
+                                      G[P_BN3B], w.bcoef + 128, w.tickets + 2, s))
       return -1;
     pa.bcoef = w.bcoef + 128;
     pa.dz = w.dz3;
@@ -4522,7 +4587,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
                          P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s)))
         return -1;
       if (bn_bwd_guard(pa, P.p[P_BN2W], P.p[P_BN2B], (double)B * g.H2 * g.W2, w.coef + 64, G[P_BN2W], G[P_BN2B],
-                       w.bcoef + 64, s))
+                       w.bcoef + 64, w.tickets + 1, s))
         return -1;
     } else {
       bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
@@ -4622,10 +4687,9 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
         // window ties and the reference routes to its first element)
         C1Args c1g = c1;
         c1g.nblk = (int)std::min<int64_t>(c1.nblk, kGuardBlocks);
-        conv1_bwd_stats_guard_kernel<<<c1g.nblk, kT, 0, s>>>(c1g, P.p[P_BN1W], P.p[P_BN1B]);
-        ABD_LAUNCH_CHECK();
-        bn_bwd_finalize_kernel<<<64, kT, 0, s>>>(w.part, c1g.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef,
-                                                 G[P_BN1W], G[P_BN1B], w.bcoef, P.p[P_BN1B]);
+        conv1_bwd_stats_guard_kernel<<<c1g.nblk, kT, 0, s>>>(
+            c1g, P.p[P_BN1W], P.p[P_BN1B],
+            GuardOut{(double)B * g.H1 * g.W1, w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, w.tickets + 0});
         ABD_LAUNCH_CHECK();
       }
     } else {
