@@ -95,9 +95,14 @@ def eval_model(name, dev, source, ref, prec="f32"):
 
 
 def envelope(ref, spread, floor_rel):
-    """Allowed |ours - ref| per epoch and metric: 3x the largest |alt - ref| the reference shows against
-    a second fp32 implementation of itself anywhere in the run, floored at floor_rel * |ref|."""
-    return np.maximum(3.0 * np.abs(spread - ref).max(axis=0, keepdims=True), floor_rel * np.abs(ref))
+    """Allowed |ours - ref| per epoch and metric: 3x the largest RELATIVE |alt - ref| / |ref| the
+    reference shows against a second fp32 implementation of itself anywhere in the run (times this
+    epoch's |ref|), floored at floor_rel * |ref|.  Relative, because fp32 divergence between two
+    implementations grows with the number of Adam steps while the losses shrink: the alt run's own
+    train-loss gap is 5.7e-6 relative at epoch 3 and 8.5e-4 at epoch 7 (badnets), so an absolute
+    run-wide maximum mostly measures which epoch the spread happened to peak in."""
+    rel = (np.abs(spread - ref) / np.maximum(np.abs(ref), 1e-12)).max(axis=0, keepdims=True)
+    return np.maximum(3.0 * rel, floor_rel) * np.abs(ref)
 
 
 # Beyond the first epoch's train loss (held to the north_star's 1e-4) the comparison is against the
