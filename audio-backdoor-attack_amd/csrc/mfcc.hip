@@ -264,9 +264,28 @@ __global__ void __launch_bounds__(kThreads) row_scale_kernel(const float* __rest
   const int64_t u = blockIdx.x;
   const int64_t row = rows ? rows[u] : u;
   const float* x = wave + row * row_stride;
-  double sx = 0.0, st = 0.0;
-  for (int64_t i = threadIdx.x; i < L; i += kThreads) sx += (double)x[i] * x[i];
-  for (int64_t i = threadIdx.x; i < inj.trig_len; i += kThreads) st += (double)inj.trig[i] * inj.trig[i];
+  // float4 loads (16-B aligned rows and trigger) with four independent double chains, so a thread
+  // keeps several loads in flight instead of one dependent load + add per element
+  auto sumsq = [&](const float* p, int64_t n) -> double {
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+    int64_t i0 = 0;
+    if (al) {
+      const float4* p4 = reinterpret_cast<const float4*>(p);
+      const int64_t n4 = n / 4;
+      for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+        const float4 v = p4[i];
+        s4[0] += (double)v.x * v.x;
+        s4[1] += (double)v.y * v.y;
+        s4[2] += (double)v.z * v.z;
+        s4[3] += (double)v.w * v.w;
+      }
+      i0 = n4 * 4;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < n; i += kThreads) s4[0] += (double)p[i] * p[i];
+    return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  };
+  double sx = sumsq(x, L), st = sumsq(inj.trig, inj.trig_len);
   __shared__ double red[2][kThreads / kWave];
   sx = abd::wave_sum_d(sx);
   st = abd::wave_sum_d(st);
