@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 O=$R/gpurun_out/$1
 mkdir -p "$O"
+python scripts/traffic_json.py --print-sha > "$O/csrc_sha1.txt"
 set -o pipefail
 step() { echo "== $1 $(date +%T)"; }
 

@@ -9,8 +9,11 @@ is exact for 16-B stores.
 Kernels are matched by their EXACT name (template arguments included, argument list dropped) and,
 for a kernel that runs more than once per step (bn_bwd_apply_kernel: BN3 then BN2), by its
 occurrence within the LAST step of the profiled run (the dispatches after the last STFT launch).
-The output records the sha1 of the libabd sources it was measured on (``csrc_sha1``): bench.py
-only uses a traffic file whose hash matches the sources it runs, and names that file per phase.
+The output records the sha1 of the libabd sources it was measured on (``csrc_sha1``), read from
+``<run dir>/csrc_sha1.txt`` (written on the GPU box by scripts/round_full.sh before it profiles);
+a run directory without that file is refused unless ``--tree-sha`` says the current tree IS the
+measured one.  bench.py only uses a traffic file whose hash matches the sources it runs, and names
+that file per phase.
 """
 import collections
 import csv
@@ -28,9 +31,12 @@ PHASE_KERNELS = {
     "stft_mel": [("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
     "db_dct": [("db_dct_mfma_kernel<3>", 0)],
     "conv1_stats": [("conv1_stats_fold_kernel", 0), ("conv1_stats_kernel", 0)],
-    "conv2_fwd": [("conv_ws_split_kernel<1, 2, 64, 1, 8, 8>", 0), ("conv_ws_kernel<1, 2, 64, 1, 8, 8>", 0)],
+    "conv2_fwd": [("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false>", 0),
+                  ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, true>", 0),
+                  ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, false>", 0)],
     "bn2_pool": [("bn_pool_fwd_kernel", 0)],
-    "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8>", 0), ("conv_ws_kernel<1, 1, 64, 1, 4, 8>", 0)],
+    "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false>", 0),
+                  ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 1, false>", 0)],
     "bn3_pool_dropout": [("bn_pool_fwd_kernel", 1)],
     "head_fwd": [("head_fwd_kernel", 0)],
     "head_mid": [("head_mid_kernel", 0)],
@@ -38,12 +44,16 @@ PHASE_KERNELS = {
     "fc1_fwd": [("gemm_nt_kernel<128, 4, 1, 32>", 0)],
     "fc1_wgrad": [("gemm_tn_kernel<128, 128>", 0)],
     "fc1_dgrad": [("gemm_nt_kernel<32, 3, 1, 32>", 0)],
-    "bn3_bwd": [("bn_bwd_apply_kernel", 0)],
-    "conv3_wgrad": [("conv_wgrad_trp_kernel<4, 32, 2, 4>", 0)],
-    "conv3_dgrad": [("conv_ws_split_kernel<0, 2, 32, 1, 4, 8>", 0), ("conv_ws_kernel<0, 2, 32, 1, 4, 8>", 0)],
-    "bn2_bwd": [("bn_bwd_apply_kernel", 1)],
-    "conv2_wgrad": [("conv_wgrad_trp_kernel<6, 64, 5, 11>", 0)],
-    "conv2_dgrad": [("conv_ws_split_kernel<0, 2, 64, 1, 8, 8>", 0), ("conv_ws_kernel<0, 2, 64, 1, 8, 8>", 0)],
+    # bn_bwd_apply_kernel runs BN3 then BN2 (round-2 head) or BN2 alone (fused head): count from the end
+    "bn3_bwd": [("bn_bwd_apply_kernel", -2)],
+    "bn2_bwd": [("bn_bwd_apply_kernel", -1)],
+    "conv3_wgrad": [("conv_wgrad_trp_kernel<4, 32, 2, 4, 3, false>", 0), ("conv_wgrad_trp_kernel<4, 32, 2, 4, 1, false>", 0)],
+    "conv3_dgrad": [("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 3, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 1, false>", 0)],
+    "conv2_wgrad": [("conv_wgrad_trp_kernel<6, 64, 5, 11, 3, false>", 0),
+                    ("conv_wgrad_trp_kernel<6, 64, 5, 11, 1, true>", 0)],
+    "conv2_dgrad": [("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 1, true>", 0)],
     "conv1_bwd_wgrad": [("conv1_wgrad_kernel<true>", 0)],
 }
 STEP_START = "stft_mel_fast_kernel<"
@@ -86,17 +96,30 @@ def last_step(d, counter):
 
 
 def pick(step, cands):
+    """First candidate present: (kernel, occurrence, value); a negative occurrence counts from the end."""
     for key, occ in cands:
         hits = [v for k, v in step if k == key]
-        if len(hits) > occ:
+        if (occ >= 0 and len(hits) > occ) or (occ < 0 and len(hits) >= -occ):
             return key, occ, hits[occ]
     return None
 
 
 def main():
-    d, dst = sys.argv[1], sys.argv[2]
+    if len(sys.argv) == 2 and sys.argv[1] == "--print-sha":
+        print(csrc_sha1())
+        return
+    args = [a for a in sys.argv[1:] if a != "--tree-sha"]
+    d, dst = args[0], args[1]
+    shaf = os.path.join(d, "csrc_sha1.txt")
+    if os.path.exists(shaf):
+        sha = open(shaf).read().strip()
+    elif "--tree-sha" in sys.argv:
+        sha = csrc_sha1()
+    else:
+        sys.exit(f"{shaf} missing: the sources this run measured are unknown (pass --tree-sha if they are "
+                 "the current tree's)")
     fetch, write = last_step(d, "FETCH_SIZE"), last_step(d, "WRITE_SIZE")
-    res = {"source": d, "csrc_sha1": csrc_sha1(),
+    res = {"source": d, "csrc_sha1": sha,
            "correction": "FETCH_SIZE x2 (gfx950 wide reads), KiB -> bytes; last profiled step", "bytes_per_launch": {},
            "detail": {}}
     for ph, cands in PHASE_KERNELS.items():

@@ -182,7 +182,25 @@ def test_daba_poison_data_end_to_end(dev, dg, tmp_path):
     assert len(hosts) == round(0.1 * 32)
     poison_files = sorted(os.listdir(out + "/poison/train/up"))
     pf = [f for f in poison_files if f.startswith("poison_")]
-    assert 0 < len(pf) <= len(hosts)
+    # How many hosts actually get poisoned follows the reference's bookkeeping quirk
+    # (daba_injection_tools.py:121-175): indices drawn over the glob order of the TRAIN files
+    # are matched in sequence against a sorted walk over ALL files, so the count depends on the
+    # filesystem's listing order and on which hosts the selection picked (0 is possible).
+    # Replay that bookkeeping and require the exact count.
+    import glob
+    random.seed(35)
+    org = [f for lab in labels for f in glob.glob(os.path.join(str(root), lab, "*.wav"))]
+    for f in random.sample(org, int(len(org) * 0.2)):
+        org.remove(f)
+    po_random, host_samples = D.my_custom_random(16, org, "up")
+    idx = sorted(dict(zip(host_samples, po_random))[h] for h in hosts)
+    expect = all_count = 0
+    for lab in labels:
+        for _ in D.get_filenames(str(root) + "/" + lab + "/", file_types="*.wav"):
+            if lab != "up" and expect < len(idx) and all_count == idx[expect]:
+                expect += 1
+            all_count += 1
+    assert len(pf) == expect <= len(hosts)
     assert os.path.exists(out + "/trigger.wav")
     test_p = [f for f in os.listdir(out + "/poison/test/up") if f.startswith("poison_")]
     assert len(test_p) > 0
