@@ -35,7 +35,7 @@ EXPORTS = (
 PHASES = ("stft_mel", "db_dct", "row_scale", "prep_weights", "conv1_stats", "conv1_bn_pool", "conv2_fwd",
           "bn2_pool", "conv3_fwd", "bn3_pool_dropout", "fc1_fwd", "fc2_loss", "metrics", "fc2_bwd", "fc1_wgrad",
           "fc1_dgrad", "bn3_bwd", "conv3_wgrad", "conv3_dgrad", "bn2_bwd", "conv2_wgrad", "conv2_dgrad",
-          "conv1_bwd_wgrad", "adam", "finalize", "head_fwd", "head_mid", "head_bwd")
+          "conv1_bwd_wgrad", "adam", "finalize", "head_fwd", "head_mid", "head_bwd", "head_dgrad")
 
 
 class Inject(C.Structure):

@@ -3344,7 +3344,8 @@ struct Work {
   float *partb3, *partb2;  // BN3 / BN2 backward-apply bias partials (read by the side stream's slab reduction)
   float* xh3;              // fused fc head: xhat of each pool3-selected element (B x flat)
   float* hslab;            // fused fc head: fc1 split-K partials (ks x B x 128)
-  float* bn3part;          // fused fc head: BN3 backward sums per row group [2][32][nrg]
+  float* part3;            // fused fc head: BN3 backward sums per (row block, feature tile, channel slot)
+  float* daT;              // fused fc head: da transposed (128 x B), head_dgrad's A operand
   uint16_t* p1s;           // conv2 plane mode: pool1 output m as exact bf16 planes [3][n_p1]
   uint16_t* dz2s;          // conv2 plane mode: BN2-backward output dz2 as planes [3][n_r2]
   unsigned* tickets;       // guarded BN fallbacks' arrival tickets (zeroed by the prep blocks)
@@ -3398,19 +3399,23 @@ int64_t c1w_blocks() {
   return n;
 }
 
-// fused fc head launch geometry (fc_head.inc): head_fwd row tiles x position splits sized for about
-// one block per CU, head_mid row groups of 16
+// fused fc head launch geometry (fc_head.inc): head_fwd row tiles of 32 x position splits of pp pooled
+// positions (pp a power of two <= 8, the smallest that keeps the grid <= 512 blocks), head_dgrad
+// 32-feature tiles x 128-row blocks
 struct HeadPlan {
-  int rt, ks, pp, nrg;
+  int rt, ks, pp, nft, nrb;
 };
 HeadPlan head_plan(const Geo& g, int64_t B) {
   HeadPlan h;
   h.rt = (int)((B + 31) / 32);
   const int P = g.flat / 32;
-  const int want = std::max(1, std::min(P, (256 + h.rt - 1) / h.rt));
-  h.pp = std::min(kHeadPP, (P + want - 1) / want);
+  static const int force = env_int("ABD_HEAD_PP", 0);
+  h.pp = 1;
+  while (h.pp < 8 && (int64_t)h.rt * ((P + h.pp - 1) / h.pp) > 512) h.pp *= 2;
+  if (force == 1 || force == 2 || force == 4 || force == 8) h.pp = force;
   h.ks = (P + h.pp - 1) / h.pp;
-  h.nrg = (int)((B + kHeadRows - 1) / kHeadRows);
+  h.nft = g.flat / 32;
+  h.nrb = (int)((B + kHeadRB - 1) / kHeadRB);
   return h;
 }
 // the train step runs the fused fc head (ABD_FC_HEAD=0 restores the round-2 launches)
@@ -3472,7 +3477,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
     const HeadPlan hp = head_plan(g, B);
     w.xh3 = F(B * g.flat);
     w.hslab = F((int64_t)hp.ks * B * 128);
-    w.bn3part = F(2LL * 32 * hp.nrg);
+    w.part3 = F((int64_t)hp.nrb * hp.nft * 64);
+    w.daT = F(128 * B);
   }
   w.p1s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_p1 * sizeof(uint16_t)));
   w.dz2s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_r2 * sizeof(uint16_t)));
@@ -3540,8 +3546,8 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.P = g.flat / 32;
   a.K = g.K;
   a.ks = hp.ks;
-  a.pp = hp.pp;
-  a.nrg = hp.nrg;
+  a.nft = hp.nft;
+  a.nrb = hp.nrb;
   a.pool = pool_args(g, 3, B);
   a.pool.r = w.r3;
   a.pool.coef = w.coef + 128;
@@ -3568,8 +3574,9 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.rowinfo = w.rowinfo;
   a.da = w.da;
   a.dp3 = w.dp3;
+  a.daT = w.daT;
   a.mask1 = w.mask1;
-  a.bn3part = w.bn3part;
+  a.part3 = w.part3;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads ? grads + net->off[i] : nullptr;
   a.g_f1w = G[P_F1W];
@@ -3590,16 +3597,26 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   return a;
 }
 
-// launch 1 (forward: pool3 + dropout1 + fc1 partials) / 2 (row head + dp3) / 3 (gradients + BN3 apply)
+// launch 1 (forward: pool3 + dropout1 + fc1 partials) / 2 (row head, then dp3 + BN3 sums) /
+// 3 (gradients + BN3 apply)
 int launch_head(int which, const HeadArgs& a, hipStream_t s) {
   if (which == 1) {
+    const dim3 grid((unsigned)((a.B + 31) / 32), (unsigned)a.ks);
+    const int pp = (a.P + a.ks - 1) / a.ks;
     abd::prof_begin(abd::PH_HEAD_FWD, s);
-    head_fwd_kernel<<<dim3((unsigned)((a.B + 31) / 32), (unsigned)a.ks), kT, 0, s>>>(a);
+    if (pp <= 1) head_fwd_kernel<1><<<grid, kT, 0, s>>>(a);
+    else if (pp <= 2) head_fwd_kernel<2><<<grid, kT, 0, s>>>(a);
+    else if (pp <= 4) head_fwd_kernel<4><<<grid, kT, 0, s>>>(a);
+    else head_fwd_kernel<8><<<grid, kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_FWD, s);
   } else if (which == 2) {
     abd::prof_begin(abd::PH_HEAD_MID, s);
-    head_mid_kernel<<<dim3((unsigned)a.nrg, 8), kT, 0, s>>>(a);
+    head_row_kernel<<<(unsigned)((a.B + kHeadRows - 1) / kHeadRows), kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_MID, s);
+    ABD_LAUNCH_CHECK();
+    abd::prof_begin(abd::PH_HEAD_DGRAD, s);
+    head_dgrad_kernel<<<dim3((unsigned)a.nft, (unsigned)a.nrb), kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_HEAD_DGRAD, s);
   } else {
     abd::prof_begin(abd::PH_HEAD_BWD, s);
     head_bwd_kernel<<<(unsigned)(a.n_w1 + a.n_w2 + 1 + a.n_apply), kT, 0, s>>>(a);

@@ -51,11 +51,13 @@ def algorithmic_work(phase, B, H0, W0, K, n_mels, T, C, L):
         "fc1_fwd": 2.0 * B * 128 * flat,
         "fc1_wgrad": 2.0 * B * 128 * flat,
         "fc1_dgrad": 2.0 * B * 128 * flat,
-        # fused fc head (fc_head.inc), priced on its dense GEMM (fp32 MFMA): head_fwd = fc1 forward
-        # (+ pool3 / BN3 / dropout1), head_mid = fc1 data gradient (+ the per-row fc2 / loss head),
+        # fused fc head (fc_head.inc), priced on its dense GEMMs (fp32 MFMA): head_fwd = fc1 forward
+        # (+ pool3 / BN3 / dropout1), head_mid = the per-row head (fc2 forward and its data
+        # gradient, + loss), head_dgrad = fc1 data gradient (+ dropout1' and BN3's sums),
         # head_bwd = fc1 weight gradient (+ fc2 gradients and BN3's backward apply)
         "head_fwd": 2.0 * B * 128 * flat,
-        "head_mid": 2.0 * B * 128 * flat,
+        "head_mid": 2.0 * 2.0 * B * 128 * K,
+        "head_dgrad": 2.0 * B * 128 * flat,
         "head_bwd": 2.0 * B * 128 * flat,
     }
     if phase in fl:

@@ -38,8 +38,9 @@ PHASE_KERNELS = {
     "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false>", 0),
                   ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 1, false>", 0)],
     "bn3_pool_dropout": [("bn_pool_fwd_kernel", 1)],
-    "head_fwd": [("head_fwd_kernel", 0)],
-    "head_mid": [("head_mid_kernel", 0)],
+    "head_fwd": [("head_fwd_kernel<4>", 0), ("head_fwd_kernel<8>", 0), ("head_fwd_kernel", 0)],
+    "head_mid": [("head_row_kernel", 0), ("head_mid_kernel", 0)],
+    "head_dgrad": [("head_dgrad_kernel", 0)],
     "head_bwd": [("head_bwd_kernel", 0)],
     "fc1_fwd": [("gemm_nt_kernel<128, 4, 1, 32>", 0)],
     "fc1_wgrad": [("gemm_tn_kernel<128, 128>", 0)],
