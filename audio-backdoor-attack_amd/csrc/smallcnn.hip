@@ -3424,6 +3424,9 @@ bool head_on() {
   return on;
 }
 
+PoolArgs pool_args(const Geo& g, int layer, int64_t B);
+int head_napply(const PoolArgs& a, int64_t B);
+
 Work layout(const abd_cnn* net, int64_t B, char* base) {
   const Geo& g = net->g;
   Work w{};
@@ -3469,7 +3472,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   w.bcoef = reinterpret_cast<BCoef*>(take(3 * 64 * sizeof(BCoef)));
   w.mask1 = reinterpret_cast<uint8_t*>(take((size_t)B * g.flat));
   w.mask2 = reinterpret_cast<uint8_t*>(take((size_t)B * 128));
-  w.partb3 = F(4096LL * 64);  // grid_for caps the apply grids at 4096 blocks
+  // grid_for caps the apply grids at 4096 blocks; the fused head's apply grid is uncapped
+  w.partb3 = F(std::max<int64_t>(4096, head_napply(pool_args(g, 3, B), B)) * 64);
   w.partb2 = F(4096LL * 64);
   w.w2fold = F(64 * 256);     // BN1 fold: conv2 weights times alpha, bias terms (double)
   w.ft2 = reinterpret_cast<double*>(take(64 * 64 * sizeof(double)));
@@ -3533,6 +3537,10 @@ PoolArgs pool_args(const Geo& g, int layer, int64_t B) {
 // extended window grid of bn_bwd_apply_kernel (windows tile the input: kernel == stride)
 int win_ext_h(const PoolArgs& a) { return std::max(a.Ho, (a.H + a.ph + a.sh - 1) / a.sh); }
 int win_ext_w(const PoolArgs& a) { return std::max(a.Wo, (a.W + a.pw + a.sw - 1) / a.sw); }
+// head_bwd_kernel's BN3 apply blocks: kHeadIT windows x 4 channels per thread, no grid stride
+int head_napply(const PoolArgs& a, int64_t B) {
+  return (int)((B * win_ext_h(a) * win_ext_w(a) * 32 / 4 + kHeadIT * kT - 1) / (kHeadIT * kT));
+}
 
 // ---- fused fc head (fc_head.inc): arguments and the three launches
 HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* grads, int64_t B,
@@ -3593,7 +3601,11 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.wx = win_ext_w(a.pool);
   a.n_w1 = 4 * ((g.flat + 31) / 32);
   a.n_w2 = 4 * ((g.K + 31) / 32) + (g.K + 128 + kHeadW2 - 1) / kHeadW2;  // fc2 weight tiles + bias sums
-  a.n_apply = grid_for(B * a.hx * a.wx * 32 / 4, 2048);
+  a.n_apply = head_napply(a.pool, B);
+  // timing ablations (results invalid): bit 0 drops the fc1 weight-gradient tiles, bit 1 the BN3 apply
+  static const int abl = env_int("ABD_HEAD_ABL", 0);
+  if (abl & 1) a.n_w1 = 0;
+  if (abl & 2) a.n_apply = 0;
   return a;
 }
 

@@ -8,13 +8,17 @@ O=$R/gpurun_out/$1
 mkdir -p "$O"
 set -o pipefail
 step() { echo "== $1 $(date +%T)"; }
+# alternating order, twice: box clock / warm-up drift shows as a rep-to-rep difference, not as a
+# precision difference
+for rep in 1 2; do
 for A in jingleback flowmur; do
-  for P in bf16 f32split; do
-    step "bench $A $P"
-    timeout -k 10 300 python bench.py --attack $A --batch 256 --gemm-precision $P --steps 100 --warmup 10 --no-cpu \
-      > "$O/bench_${A}_${P}.json" 2> "$O/bench_${A}_${P}.err" || { tail -20 "$O/bench_${A}_${P}.err"; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d['value'])" "$O/bench_${A}_${P}.json"
+  for P in f32split bf16; do
+    step "bench $A $P rep $rep"
+    timeout -k 10 300 python bench.py --attack $A --batch 256 --gemm-precision $P --steps 200 --warmup 20 --no-cpu \
+      > "$O/bench_${A}_${P}_$rep.json" 2> "$O/bench_${A}_${P}_$rep.err" || { tail -20 "$O/bench_${A}_${P}_$rep.err"; exit 1; }
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d['value'])" "$O/bench_${A}_${P}_$rep.json"
   done
+done
 done
 cd /tmp && export TMPDIR=/tmp
 for A in jingleback flowmur; do
