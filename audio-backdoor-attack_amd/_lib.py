@@ -57,7 +57,7 @@ class Effect(C.Structure):
     _fields_ = [("kind", C.c_int), ("p", C.c_float * 8)]
 
 
-FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER, FX_CHORUS, FX_REVERB = 0, 1, 2, 3, 4, 5
+FX_GAIN, FX_DISTORTION, FX_LADDER, FX_PHASER, FX_CHORUS, FX_REVERB, FX_PITCHSHIFT = 0, 1, 2, 3, 4, 5, 6
 PREC_F32, PREC_BF16, PREC_F32_SPLIT = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "bf16": PREC_BF16, "f32split": PREC_F32_SPLIT}
 

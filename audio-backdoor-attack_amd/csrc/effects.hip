@@ -85,6 +85,12 @@ __device__ __forceinline__ float undenorm(float v) {
   return __fsub_rn(v, 0.1f);
 }
 
+// effects [0, e) applied to one sample; only Gain / Distortion may precede a Chorus
+__device__ __forceinline__ float memoryless_prefix(const FxDev& d, int e, float x) {
+  for (int q = 0; q < e; ++q) x = d.kind[q] == ABD_FX_DISTORTION ? tanhf(x * d.gain[q]) : x * d.gain[q];
+  return x;
+}
+
 __device__ __forceinline__ float run_chain(const FxDev& d, Chain& c, float x, int64_t t) {
   for (int e = 0; e < d.n; ++e) {
     switch (d.kind[e]) {
@@ -114,7 +120,10 @@ __device__ __forceinline__ float run_chain(const FxDev& d, Chain& c, float x, in
         const int di = (int)floorf(dl);
         const float fr = dl - (float)di;
         const int64_t s1 = t - di, s2 = t - di - 1;
-        const float v1 = s1 >= 0 ? c.x[s1] : 0.0f, v2 = s2 >= 0 ? c.x[s2] : 0.0f;
+        // the delay line holds the chorus's own input: the clip through the (memoryless) effects
+        // before it -- Gain / Distortion, checked at board creation; zeros before t = 0
+        const float v1 = s1 >= 0 ? memoryless_prefix(d, e, c.x[s1]) : 0.0f;
+        const float v2 = s2 >= 0 ? memoryless_prefix(d, e, c.x[s2]) : 0.0f;
         const float wet = __fadd_rn(v1, __fmul_rn(fr, __fsub_rn(v2, v1)));
         x = __fadd_rn(__fmul_rn(wet, d.cwet), __fmul_rn(x, d.cdry));
         break;
@@ -266,6 +275,241 @@ __global__ void __launch_bounds__(kThreads) board_fast_kernel(FxDev d, int gi, i
   }
 }
 
+// ---- PitchShift stage (styles 0 and 3) -------------------------------------------------------
+// pedalboard.PitchShift is Rubber Band R2 in real-time mode: a phase-vocoder time stretch by
+// r = 2^(semitones/12) followed by a resample by 1/r.  Rubber Band publishes no bit-level spec, so
+// the stage is a phase vocoder of that structure whose every constant is defined in
+// oracle/effects.py (pitch_shift) -- parity unpinned against pedalboard, 1e-4 against the oracle.
+// Five launches per board application, each over the whole batch:
+//   analysis   grid (frame pairs, clips): two windowed real frames packed into one complex
+//              N-point FFT (Stockham radix-4 [+2] in LDS), split into the two half spectra,
+//              stored as (|X|, arg X) per bin; an all-zero frame stores exact zeros (the oracle's
+//              rfft of a zero frame), not the packing's rounding cross-talk
+//   phase      thread per (clip, bin): the phase-vocoder recursion over the frames, in place
+//              -> Y = |X| e^{i phi_s}; every phase increment reduced mod 2 pi with the k h mod N
+//              terms formed in integers, so the fp32 accumulator stays within [-pi, pi]
+//   synthesis  grid (frame pairs, clips): two Hermitian spectra packed into one inverse FFT,
+//              real / imaginary parts = the two frames, times the window
+//   ola        thread per stretched sample: the <= 4 overlapping frames summed in frame order,
+//              divided by sum w^2
+//   resample   thread per output sample: windowed-sinc interpolation at n r (position in double)
+// Work per 1 s clip at 16 kHz: 117 frames of N = 1024 each way -- HBM / latency-bound, off the
+// training step (jingleback poisons once, jingleback.py:69-78).
+struct PitchDev {
+  int N, K, Hs, Tmax;
+  double r;
+  float fc, W;
+  const int* ia;       // analysis centres, Tmax
+  const float* win;    // periodic Hann, N
+  const float2* tw;    // exp(-2 pi i e / N), e < N
+};
+
+constexpr int kPitchThreads = 256;
+constexpr float kTwoPi = 6.283185307179586f;
+
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float princargf(float x) { return x - kTwoPi * rintf(x * (1.0f / kTwoPi)); }
+
+// forward FFT of a[0..N) (LDS), b scratch; returns the buffer holding the result
+template <int N>
+__device__ float2* fft_lds(float2* a, float2* b, const float2* __restrict__ tw) {
+  float2* src = a;
+  float2* dst = b;
+  int ns = 1;
+  for (; ns * 4 <= N; ns *= 4) {
+    const int tstep = N / (4 * ns);
+    for (int j = threadIdx.x; j < N / 4; j += kPitchThreads) {
+      const int k = j & (ns - 1);
+      float2 v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = src[j + r * (N / 4)];
+        if (r > 0) v[r] = cmulf(v[r], tw[k * r * tstep]);
+      }
+      const float2 t0 = make_float2(v[0].x + v[2].x, v[0].y + v[2].y);
+      const float2 t1 = make_float2(v[0].x - v[2].x, v[0].y - v[2].y);
+      const float2 t2 = make_float2(v[1].x + v[3].x, v[1].y + v[3].y);
+      const float2 t3 = make_float2(v[1].x - v[3].x, v[1].y - v[3].y);
+      const int d = (j - k) * 4 + k;
+      dst[d] = make_float2(t0.x + t2.x, t0.y + t2.y);
+      dst[d + ns] = make_float2(t1.x + t3.y, t1.y - t3.x);       // t1 - i t3
+      dst[d + 2 * ns] = make_float2(t0.x - t2.x, t0.y - t2.y);
+      dst[d + 3 * ns] = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
+    }
+    __syncthreads();
+    float2* tmp = src;
+    src = dst;
+    dst = tmp;
+  }
+  if (ns < N) {  // one radix-2 pass (N = 2 * 4^m)
+    const int tstep = N / (2 * ns);
+    for (int j = threadIdx.x; j < N / 2; j += kPitchThreads) {
+      const int k = j & (ns - 1);
+      const float2 v0 = src[j], v1 = cmulf(src[j + N / 2], tw[k * tstep]);
+      const int d = (j - k) * 2 + k;
+      dst[d] = make_float2(v0.x + v1.x, v0.y + v1.y);
+      dst[d + ns] = make_float2(v0.x - v1.x, v0.y - v1.y);
+    }
+    __syncthreads();
+    src = dst;
+  }
+  return src;
+}
+
+template <int N>
+__global__ void __launch_bounds__(kPitchThreads) pitch_analysis_kernel(PitchDev p, const float* __restrict__ in,
+                                                                      int64_t in_stride, const int32_t* __restrict__ rows,
+                                                                      int L, int T, float2* __restrict__ spec) {
+  __shared__ float2 bufa[N], bufb[N];
+  const int64_t u = blockIdx.y;
+  const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
+  const float* x = in + (rows ? (int64_t)rows[u] : u) * in_stride;
+  const int c0 = p.ia[t0] - N / 2, c1 = t1 < T ? p.ia[t1] - N / 2 : 0;
+  bool nz0 = false, nz1 = false;
+  for (int n = threadIdx.x; n < N; n += kPitchThreads) {
+    const int s0 = c0 + n, s1 = c1 + n;
+    const float a = (s0 >= 0 && s0 < L) ? x[s0] : 0.0f;
+    const float b = (t1 < T && s1 >= 0 && s1 < L) ? x[s1] : 0.0f;
+    nz0 |= a != 0.0f;
+    nz1 |= b != 0.0f;
+    const float w = p.win[n];
+    bufa[n] = make_float2(a * w, b * w);
+  }
+  nz0 = __syncthreads_or(nz0);
+  nz1 = __syncthreads_or(nz1);
+  const float2* Z = fft_lds<N>(bufa, bufb, p.tw);
+  constexpr int K = N / 2 + 1;
+  float2* s0 = spec + ((int64_t)u * T + t0) * K;
+  float2* s1 = spec + ((int64_t)u * T + t1) * K;
+  for (int k = threadIdx.x; k < K; k += kPitchThreads) {
+    const float2 zk = Z[k], zn = Z[(N - k) & (N - 1)];
+    // A = (Z[k] + conj Z[N-k]) / 2, B = (Z[k] - conj Z[N-k]) / 2i
+    const float ar = 0.5f * (zk.x + zn.x), ai = 0.5f * (zk.y - zn.y);
+    const float br = 0.5f * (zk.y + zn.y), bi = -0.5f * (zk.x - zn.x);
+    const float ma = sqrtf(ar * ar + ai * ai), mb = sqrtf(br * br + bi * bi);
+    s0[k] = nz0 ? make_float2(ma, ma == 0.0f ? 0.0f : atan2f(ai, ar)) : make_float2(0.0f, 0.0f);
+    if (t1 < T) s1[k] = nz1 ? make_float2(mb, mb == 0.0f ? 0.0f : atan2f(bi, br)) : make_float2(0.0f, 0.0f);
+  }
+}
+
+__global__ void __launch_bounds__(kPitchThreads) pitch_phase_kernel(PitchDev p, int T, float2* __restrict__ spec) {
+  const int k = blockIdx.x * kPitchThreads + threadIdx.x;
+  if (k >= p.K) return;
+  float2* s = spec + (int64_t)blockIdx.y * T * p.K + k;
+  const int N = p.N;
+  const float adv = kTwoPi * (float)((k * p.Hs) % N) / (float)N;  // 2 pi (k Hs mod N) / N
+  float pa_prev = 0.0f, ps = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    const float2 mp = s[(int64_t)t * p.K];
+    if (t == 0) {
+      ps = mp.y;
+    } else {
+      const int h = p.ia[t] - p.ia[t - 1];
+      const float omh = kTwoPi * (float)((int)(((int64_t)k * h) % N)) / (float)N;
+      const float dphi = princargf(mp.y - pa_prev - omh);
+      ps = princargf(ps + adv + ((float)p.Hs / (float)h) * dphi);
+    }
+    pa_prev = mp.y;
+    float sn, cs;
+    sincosf(ps, &sn, &cs);
+    s[(int64_t)t * p.K] = make_float2(mp.x * cs, mp.x * sn);
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(kPitchThreads) pitch_synthesis_kernel(PitchDev p, int T, const float2* __restrict__ spec,
+                                                                       float* __restrict__ frames) {
+  __shared__ float2 bufa[N], bufb[N];
+  constexpr int K = N / 2 + 1;
+  const int64_t u = blockIdx.y;
+  const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
+  const float2* s0 = spec + ((int64_t)u * T + t0) * K;
+  const float2* s1 = spec + ((int64_t)u * T + t1) * K;
+  for (int k = threadIdx.x; k < N; k += kPitchThreads) {
+    const int kk = k <= N / 2 ? k : N - k;
+    float2 y0 = s0[kk], y1 = t1 < T ? s1[kk] : make_float2(0.0f, 0.0f);
+    if (kk == 0 || kk == N / 2) {  // irfft: the imaginary parts of DC and Nyquist are dropped
+      y0.y = 0.0f;
+      y1.y = 0.0f;
+    }
+    if (k > N / 2) {  // Hermitian extension
+      y0.y = -y0.y;
+      y1.y = -y1.y;
+    }
+    // Z = Y0 + i Y1; inverse FFT as conj(FFT(conj Z)) / N
+    bufa[k] = make_float2(y0.x - y1.y, -(y0.y + y1.x));
+  }
+  __syncthreads();
+  const float2* R = fft_lds<N>(bufa, bufb, p.tw);
+  float* f0 = frames + ((int64_t)u * T + t0) * N;
+  float* f1 = frames + ((int64_t)u * T + t1) * N;
+  const float inv = 1.0f / (float)N;
+  for (int n = threadIdx.x; n < N; n += kPitchThreads) {
+    const float w = p.win[n];
+    f0[n] = (R[n].x * inv) * w;
+    if (t1 < T) f1[n] = (-R[n].y * inv) * w;
+  }
+}
+
+__global__ void __launch_bounds__(kPitchThreads) pitch_ola_kernel(PitchDev p, int T, int Ls, const float* __restrict__ frames,
+                                                                 float* __restrict__ ys) {
+  const int j = blockIdx.x * kPitchThreads + threadIdx.x;
+  if (j >= Ls) return;
+  const int64_t u = blockIdx.y;
+  const int N = p.N, H = p.Hs;
+  // frames t with 0 <= j - t H + N/2 < N
+  const int tlo = max(0, (j + N / 2 - N + 1 + H - 1) / H), thi = min(T - 1, (j + N / 2) / H);
+  float acc = 0.0f, ws = 0.0f;
+  for (int t = tlo; t <= thi; ++t) {
+    const int i = j - t * H + N / 2;
+    acc += frames[((int64_t)u * T + t) * N + i];
+    const float w = p.win[i];
+    ws += w * w;
+  }
+  ys[u * Ls + j] = ws > 1e-6f ? acc / ws : 0.0f;
+}
+
+__global__ void __launch_bounds__(kPitchThreads) pitch_resample_kernel(PitchDev p, int Ls, const float* __restrict__ ys,
+                                                                      int L, float* __restrict__ out, int64_t out_stride) {
+  const int n = blockIdx.x * kPitchThreads + threadIdx.x;
+  if (n >= L) return;
+  const int64_t u = blockIdx.y;
+  const double pos = (double)n * p.r;
+  const int jlo = max(0, (int)ceil(pos - (double)p.W)), jhi = min(Ls - 1, (int)floor(pos + (double)p.W));
+  const float* y = ys + u * Ls;
+  const float f2 = 2.0f * p.fc;
+  float acc = 0.0f;
+  for (int j = jlo; j <= jhi; ++j) {
+    const float d = (float)(pos - (double)j);
+    if (fabsf(d) < p.W) {
+      const float z = f2 * d;
+      const float sc = z == 0.0f ? 1.0f : sinpif(z) / (3.14159265358979f * z);
+      acc += y[j] * (f2 * sc * 0.5f * (1.0f + cospif(d / p.W)));
+    }
+  }
+  out[u * out_stride + n] = acc;
+}
+
+// workspace regions of the pitch stage for `batch` clips of `length` samples (256-B aligned)
+struct PitchWs {
+  size_t spec, frames, ys, pout, total;
+};
+inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+PitchWs pitch_ws(const PitchDev& p, int64_t batch, int64_t length, bool need_out) {
+  const double r = p.r;
+  const int64_t Ls = (int64_t)std::ceil((double)length * r);
+  const int64_t T = (Ls + p.Hs - 1) / p.Hs + 1;
+  PitchWs w{};
+  w.spec = 0;
+  w.frames = w.spec + align256((size_t)batch * T * p.K * sizeof(float2));
+  w.ys = w.frames + align256((size_t)batch * T * p.N * sizeof(float));
+  w.pout = w.ys + align256((size_t)batch * Ls * sizeof(float));
+  w.total = w.pout + (need_out ? align256((size_t)batch * length * sizeof(float)) : 0);
+  return w;
+}
+
 // ---- host-side JUCE restatements (float, like the plugins) --------------------------------
 float decibels_to_gain(float db) { return db > -100.0f ? std::pow(10.0f, db * 0.05f) : 0.0f; }
 
@@ -277,6 +521,9 @@ struct abd_style_board {
   int sample_rate;
   int64_t max_length;
   bool reverb = false;
+  bool pitch = false;  // a PitchShift opens the board: run as the pitch stage, then dev's chain
+  PitchDev pd{};
+  void* pblock = nullptr;  // pitch tables: ia, window, twiddles
 };
 
 extern "C" {
@@ -285,6 +532,36 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
                            abd_style_board** board) {
   ABD_CHECK(board && (fx || n == 0), ABD_E_INVALID, "NULL argument");
   ABD_CHECK(n >= 0 && n <= kMaxFx && sample_rate > 0 && max_length >= 0, ABD_E_INVALID, "bad board parameters");
+  // PitchShift: the board's pitch stage (first effect only); the rest is the sample chain
+  PitchDev pd{};
+  const bool pitch = n > 0 && fx[0].kind == ABD_FX_PITCHSHIFT;
+  std::vector<int> ia;
+  std::vector<float> win;
+  std::vector<float2> tw;
+  if (pitch) {
+    const double st = fx[0].p[0];
+    ABD_CHECK(std::isfinite(st) && std::fabs(st) <= 24.0, ABD_E_INVALID, "PitchShift semitones %g outside [-24, 24]", st);
+    pd.r = std::pow(2.0, st / 12.0);
+    pd.N = sample_rate < 32000 ? 1024 : 2048;
+    pd.K = pd.N / 2 + 1;
+    pd.Hs = pd.N / 4;
+    pd.fc = (float)(0.475 / std::max(pd.r, 1.0));
+    pd.W = (float)(8.0 / (2.0 * (0.475 / std::max(pd.r, 1.0))));
+    const int64_t Ls = (int64_t)std::ceil((double)max_length * pd.r);
+    pd.Tmax = (int)((Ls + pd.Hs - 1) / pd.Hs + 1);
+    ia.resize(pd.Tmax);
+    for (int t = 0; t < pd.Tmax; ++t) ia[t] = (int)std::floor((double)t * pd.Hs / pd.r + 0.5);
+    win.resize(pd.N);
+    tw.resize(pd.N);
+    for (int i = 0; i < pd.N; ++i) {
+      win[i] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * i / pd.N));
+      tw[i] = make_float2((float)std::cos(-2.0 * M_PI * i / pd.N), (float)std::sin(-2.0 * M_PI * i / pd.N));
+    }
+    ++fx;
+    --n;
+  }
+  for (int e = 0; e < n; ++e)
+    ABD_CHECK(fx[e].kind != ABD_FX_PITCHSHIFT, ABD_E_UNSUPPORTED, "PitchShift is accelerated as the first effect of a board only");
   FxDev d{};
   d.n = n;
   int nlad = 0, nph = 0, nrv = 0;
@@ -356,7 +633,9 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
         break;
       }
       case ABD_FX_CHORUS: {
-        ABD_CHECK(e == 0, ABD_E_UNSUPPORTED, "Chorus must be the first effect of a board (it reads the clip's history)");
+        for (int q = 0; q < e; ++q)
+          ABD_CHECK(fx[q].kind == ABD_FX_GAIN || fx[q].kind == ABD_FX_DISTORTION, ABD_E_UNSUPPORTED,
+                    "only Gain / Distortion may precede a Chorus (its delay line re-applies them to the history)");
         const float rate = f.p[0], depth = f.p[1], centre = f.p[2], feedback = f.p[3], mix = f.p[4];
         ABD_CHECK(feedback == 0.0f, ABD_E_UNSUPPORTED, "Chorus feedback != 0 is not accelerated");
         // juce::dsp::Chorus: sine LFO at the sample rate (float phase), x depth * 0.5, delay
@@ -423,6 +702,28 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
     abd::set_last_error("style board table upload: %s", hipGetErrorString(e));
     return (int)e;
   }
+  if (pitch) {
+    const size_t nb = ia.size() * sizeof(int) + win.size() * sizeof(float) + tw.size() * sizeof(float2);
+    e = hipMalloc(&b->pblock, nb);
+    char* pb = static_cast<char*>(b->pblock);
+    if (e == hipSuccess) e = hipMemcpy(pb, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(pb + tw.size() * sizeof(float2), win.data(), win.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(pb + tw.size() * sizeof(float2) + win.size() * sizeof(float), ia.data(), ia.size() * sizeof(int),
+                    hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (b->pblock) (void)hipFree(b->pblock);
+      (void)hipFree(b->block);
+      delete b;
+      abd::set_last_error("pitch table upload: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    pd.tw = reinterpret_cast<const float2*>(pb);
+    pd.win = reinterpret_cast<const float*>(pb + tw.size() * sizeof(float2));
+    pd.ia = reinterpret_cast<const int*>(pb + tw.size() * sizeof(float2) + win.size() * sizeof(float));
+    b->pitch = true;
+    b->pd = pd;
+  }
   d.lut = b->block;
   d.pG = b->block + kLut + 1;
   d.pG_len = (int64_t)G.size();
@@ -438,13 +739,20 @@ int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t
 void abd_style_board_destroy(abd_style_board* board) {
   if (!board) return;
   if (board->block) (void)hipFree(board->block);
+  if (board->pblock) (void)hipFree(board->pblock);
   delete board;
 }
 
+// workspace: [pitch stage regions (pitch_ws)][reverb buffers]
+static size_t pitch_bytes(const abd_style_board* b, int64_t batch, int64_t length) {
+  return b->pitch ? pitch_ws(b->pd, batch, length, b->dev.n > 0).total : 0;
+}
 size_t abd_style_board_workspace_bytes(const abd_style_board* board, int64_t batch) {
-  if (!board || !board->reverb || batch <= 0) return 0;
+  if (!board || batch <= 0) return 0;
+  const size_t pb = pitch_bytes(board, batch, board->max_length);
+  if (!board->reverb) return pb;
   const int64_t pitch = (batch + 63) / 64 * 64;
-  return (size_t)board->dev.rstride * (size_t)pitch * sizeof(float);
+  return pb + (size_t)board->dev.rstride * (size_t)pitch * sizeof(float);
 }
 
 int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride, const int32_t* rows,
@@ -461,6 +769,39 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
   const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const FxDev& d = board->dev;
+  // reverb buffers sit past the pitch regions (sized for max_length, like workspace_bytes)
+  char* rws = static_cast<char*>(workspace) + pitch_bytes(board, batch, board->max_length);
+  if (board->pitch) {
+    const PitchDev& p = board->pd;
+    ABD_CHECK(length <= INT32_MAX / 4 && batch <= 65535, ABD_E_INVALID, "pitch stage: batch %lld / length %lld too large",
+              (long long)batch, (long long)length);
+    const PitchWs w = pitch_ws(p, batch, length, d.n > 0);
+    const int Ls = (int)std::ceil((double)length * p.r);
+    const int T = (Ls + p.Hs - 1) / p.Hs + 1;
+    ABD_CHECK(T <= p.Tmax, ABD_E_INVALID, "pitch stage: %d frames > %d", T, p.Tmax);
+    char* base = static_cast<char*>(workspace);
+    float2* spec = reinterpret_cast<float2*>(base + w.spec);
+    float* frames = reinterpret_cast<float*>(base + w.frames);
+    float* ys = reinterpret_cast<float*>(base + w.ys);
+    float* pout = d.n > 0 ? reinterpret_cast<float*>(base + w.pout) : out;
+    const int64_t pstride = d.n > 0 ? length : out_stride;
+    const dim3 gpair((unsigned)((T + 1) / 2), (unsigned)batch);
+    if (p.N == 1024) pitch_analysis_kernel<1024><<<gpair, kPitchThreads, 0, s>>>(p, in, in_stride, rows, (int)length, T, spec);
+    else pitch_analysis_kernel<2048><<<gpair, kPitchThreads, 0, s>>>(p, in, in_stride, rows, (int)length, T, spec);
+    pitch_phase_kernel<<<dim3((unsigned)((p.K + kPitchThreads - 1) / kPitchThreads), (unsigned)batch), kPitchThreads, 0, s>>>(
+        p, T, spec);
+    if (p.N == 1024) pitch_synthesis_kernel<1024><<<gpair, kPitchThreads, 0, s>>>(p, T, spec, frames);
+    else pitch_synthesis_kernel<2048><<<gpair, kPitchThreads, 0, s>>>(p, T, spec, frames);
+    pitch_ola_kernel<<<dim3((unsigned)((Ls + kPitchThreads - 1) / kPitchThreads), (unsigned)batch), kPitchThreads, 0, s>>>(
+        p, T, Ls, frames, ys);
+    pitch_resample_kernel<<<dim3((unsigned)((length + kPitchThreads - 1) / kPitchThreads), (unsigned)batch), kPitchThreads,
+                            0, s>>>(p, Ls, ys, (int)length, pout, pstride);
+    ABD_LAUNCH_CHECK();
+    if (d.n == 0) return ABD_OK;
+    in = pout;  // the sample chain reads the shifted clips in batch order
+    in_stride = length;
+    rows = nullptr;
+  }
   // canonical order Gain < Distortion < Ladder < Phaser (kinds 0..3), each at most once -> fast path
   int mask = 0, last = -1, gi = 0, di = 0;
   bool canon = getenv("ABD_FX_GENERIC") == nullptr;
@@ -474,7 +815,7 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
   }
   if (!canon) {
     board_kernel<<<grid, kThreads, 0, s>>>(d, in, in_stride, rows, batch, length, out, out_stride,
-                                           board->reverb ? static_cast<float*>(workspace) : nullptr,
+                                           board->reverb ? reinterpret_cast<float*>(rws) : nullptr,
                                            (batch + 63) / 64 * 64);
   } else {
     switch (mask) {

@@ -1,5 +1,5 @@
 """Drop-in for utils/styles_trigger.py: the pedalboard boards run as libabd kernels (csrc/effects.hip);
-PitchShift boards (styles 0 and 3) raise AbdError."""
+PitchShift (styles 0 and 3) runs as the board's phase-vocoder pitch stage."""
 import os
 import sys
 

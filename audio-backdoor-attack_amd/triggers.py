@@ -4,7 +4,7 @@
 * Ultrasonic ``GenerateTrigger`` / ``TriggerInfeasible``        utils/ultra_trigger.py:8-111
 * FlowMur  ``deploy_trigger_to_waveform``                       utils/flowmur_generate_trigger.py:49-62
 * DABA     ``single_trigger_injection_db`` on int16 arrays      utils/daba_selection_tools.py:24-39
-* JingleBack ``get_boards`` / ``poison_style``                  utils/styles_trigger.py:8-53 (libabd effects kernels; PitchShift raises)
+* JingleBack ``get_boards`` / ``poison_style``                  utils/styles_trigger.py:8-53 (libabd effects kernels + pitch stage)
 
 Trigger *construction* is a one-off host computation (microseconds, once per run);
 trigger *application* per batch happens inside libabd's feature kernel
@@ -219,7 +219,8 @@ class Phaser(_Effect):
 
 
 class Chorus(_Effect):
-    """pedalboard.Chorus (juce::dsp::Chorus); feedback must be 0 and it must open the board."""
+    """pedalboard.Chorus (juce::dsp::Chorus); feedback must be 0, and only Gain / Distortion (after
+    an opening PitchShift) may precede it in a board."""
     kind = L.FX_CHORUS
 
     def __init__(self, rate_hz=1.0, depth=0.25, centre_delay_ms=7.0, feedback=0.0, mix=0.5):
@@ -247,8 +248,18 @@ class _Unsupported(_Effect):
         self.args, self.kwargs = a, k
 
 
-class PitchShift(_Unsupported):
-    """Rubber Band time-stretching: not restated (no public bit-level spec); boards with it raise."""
+class PitchShift(_Effect):
+    """pedalboard.PitchShift(semitones) (utils/styles_trigger.py:13,29): Rubber Band's structure -- a
+    phase-vocoder stretch by r = 2^(semitones/12), then a resample by 1/r -- as the board's pitch
+    stage (csrc/effects.hip).  Rubber Band has no public bit-level spec: the stage is the phase
+    vocoder oracle/effects.py defines (parity unpinned against pedalboard).  First effect only."""
+    kind = L.FX_PITCHSHIFT
+
+    def __init__(self, semitones=0.0):
+        self.semitones = float(semitones)
+
+    def params(self):
+        return [self.semitones]
 
 
 class Pedalboard:
@@ -271,7 +282,7 @@ class Pedalboard:
             bad = [type(p).__name__ for p in self.plugins if isinstance(p, _Unsupported)]
             if bad:
                 raise L.AbdError(f"pedalboard effects {bad} are not accelerated (SURVEY.md §8 a8: Gain, Distortion, "
-                                 "LadderFilter, Phaser, Chorus and Reverb are; styles 1, 2, 4 and the default 5 run)")
+                                 "LadderFilter, Phaser, Chorus, Reverb and PitchShift are; every style runs)")
             fx = (L.Effect * max(len(self.plugins), 1))()
             for i, p in enumerate(self.plugins):
                 fx[i].kind = p.kind
@@ -317,7 +328,7 @@ class Pedalboard:
 
 
 def get_boards():
-    """utils/styles_trigger.py:8-48: the six styles (0 and 3 need PitchShift, which is not accelerated)."""
+    """utils/styles_trigger.py:8-48: the six styles (PitchShift in styles 0 and 3: see PitchShift)."""
     return [
         Pedalboard([PitchShift(semitones=10)]),
         Pedalboard([Distortion(drive_db=30)]),

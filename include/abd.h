@@ -177,13 +177,19 @@ int abd_resample_f32(const abd_resample_plan* plan, const float* in, int64_t in_
  *               p2 resonance, p3 drive                        (at most one per board)
  *   PHASER      p0 rate_hz, p1 depth, p2 centre_frequency_hz, p3 feedback, p4 mix (one per board)
  *   CHORUS      p0 rate_hz, p1 depth, p2 centre_delay_ms, p3 feedback (must be 0), p4 mix
- *               (first effect of the board: its delay line reads the clip itself)
+ *               (its delay line reads the chain's input history: only memoryless effects
+ *               may precede it, see below)
  *   REVERB      p0 room_size, p1 damping, p2 wet_level, p3 dry_level, p4 width, p5 freeze_mode
  *               (juce::Reverb mono, JUCE_UNDENORMALISE as on x86 builds; one per board;
  *               its comb / allpass buffers live in the caller's workspace)
- * PitchShift (Rubber Band) is not accelerated (ABD_E_UNSUPPORTED). */
+ *   PITCHSHIFT  p0 semitones                                  (first effect of the board, at most one)
+ *               pedalboard.PitchShift is Rubber Band (R2: phase-vocoder stretch by r = 2^(st/12),
+ *               then a resample by 1/r); no bit-level spec is public, so this is a phase vocoder of
+ *               the same structure defined in oracle/effects.py (pitch_shift): parity unpinned.
+ *   Effects between the board's start (after a PitchShift) and a Chorus must be memoryless (Gain,
+ *   Distortion): the chorus delay line re-applies them to the history it reads. */
 enum { ABD_FX_GAIN = 0, ABD_FX_DISTORTION = 1, ABD_FX_LADDER = 2, ABD_FX_PHASER = 3, ABD_FX_CHORUS = 4,
-       ABD_FX_REVERB = 5 };
+       ABD_FX_REVERB = 5, ABD_FX_PITCHSHIFT = 6 };
 typedef struct abd_effect {
   int kind;
   float p[8];
@@ -192,7 +198,8 @@ typedef struct abd_style_board abd_style_board;
 int abd_style_board_create(const abd_effect* fx, int n, int sample_rate, int64_t max_length,
                            abd_style_board** board);
 void abd_style_board_destroy(abd_style_board* board);
-/* bytes of workspace abd_style_board_apply needs for `batch` clips (0 without a Reverb) */
+/* bytes of workspace abd_style_board_apply needs for `batch` clips of up to max_length samples
+ * (0 without a Reverb or a PitchShift) */
 size_t abd_style_board_workspace_bytes(const abd_style_board* board, int64_t batch);
 /* out[u] = board(in[rows ? rows[u] : u]) for `length` samples (<= max_length) */
 int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t in_stride,

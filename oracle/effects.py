@@ -217,3 +217,95 @@ def style4(x, sr=16000):
     y = chorus(x, sr, centre_delay_ms=15.0)
     y = np.tanh(y * db_to_gain(20.0))
     return reverb(y, sr, room_size=0.6)
+
+
+# ------------------------------------------------------------------ PitchShift (styles 0, 3)
+# pedalboard.PitchShift wraps Rubber Band (R2 engine, real-time mode): a phase-vocoder time
+# stretch by r = 2^(semitones/12) followed by a resample by 1/r.  Rubber Band is not importable
+# here and has no published bit-level specification (phase laminarity, transient detection and its
+# resampler are implementation details), so this is OUR pitch shifter in the same structure, and the
+# device path (csrc/effects.hip, pitch stage) restates exactly this -- parity unpinned against
+# pedalboard.  Every constant below is part of the definition:
+#   N = 1024 (sr < 32 kHz) else 2048, synthesis hop Hs = N / 4, periodic Hann window w;
+#   synthesis frame t is centred at t Hs in the stretched signal (length Ls = ceil(L r)),
+#   T = ceil(Ls / Hs) + 1 frames; analysis frame t is centred at ia_t = floor(t Hs / r + 1/2) in
+#   the input (zero outside [0, L)), so stretched sample j <-> input time j / r;
+#   phase vocoder (no phase locking): phi_s[0] = phi_a[0]; for t >= 1, h = ia_t - ia_{t-1},
+#     dphi = princarg(phi_a[t] - phi_a[t-1] - 2 pi ((k h) mod N) / N),
+#     phi_s[t] = princarg(phi_s[t-1] + 2 pi ((k Hs) mod N) / N + (Hs / h) dphi),
+#     the phase of an exactly-zero bin is 0; Y_t = |X_t| e^{i phi_s}, irfft (imaginary parts of
+#     bins 0 and N/2 dropped), times w, overlap-added and divided by sum_t w^2;
+#   resample: out[n] = sum_j ys[j] h(n r - j), h(x) = 2 fc sinc(2 fc x) (1 + cos(pi x / W)) / 2 on
+#     |x| < W, fc = 0.475 / max(r, 1), W = 8 / (2 fc).
+def pitch_params(sr, semitones):
+    r = 2.0 ** (float(semitones) / 12.0)
+    N = 1024 if sr < 32000 else 2048
+    return r, N, N // 4
+
+
+def pitch_frames(length, r, Hs):
+    Ls = int(math.ceil(length * r))
+    T = -(-Ls // Hs) + 1
+    ia = np.floor(np.arange(T) * Hs / r + 0.5).astype(np.int64)
+    return Ls, T, ia
+
+
+def _princarg(x):
+    return x - 2 * np.pi * np.rint(x / (2 * np.pi))
+
+
+def pitch_shift(x, sr, semitones=10.0):
+    """(B, L) -> (B, L) float64."""
+    x = np.asarray(x, dtype=np.float64)
+    B, L = x.shape
+    r, N, Hs = pitch_params(sr, semitones)
+    Ls, T, ia = pitch_frames(L, r, Hs)
+    K = N // 2 + 1
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(N) / N)
+    xp = np.zeros((B, L + 2 * N))
+    xp[:, N:N + L] = x
+    idx = (ia[:, None] - N // 2 + np.arange(N)[None, :]) + N            # (T, N) into xp
+    fr = xp[:, np.clip(idx, 0, L + 2 * N - 1)] * ((idx >= N) & (idx < N + L))[None] * w
+    X = np.fft.rfft(fr, axis=2)                                         # (B, T, K)
+    mag = np.abs(X)
+    pha = np.where(mag == 0, 0.0, np.angle(X))
+    k = np.arange(K)
+    ps = np.empty_like(pha)
+    ps[:, 0] = pha[:, 0]
+    for t in range(1, T):
+        h = int(ia[t] - ia[t - 1])
+        dphi = _princarg(pha[:, t] - pha[:, t - 1] - 2 * np.pi * ((k * h) % N) / N)
+        ps[:, t] = _princarg(ps[:, t - 1] + 2 * np.pi * ((k * Hs) % N) / N + (Hs / h) * dphi)
+    Y = mag * np.exp(1j * ps)
+    y = np.fft.irfft(Y, n=N, axis=2) * w                                # (B, T, N)
+    ys = np.zeros((B, Ls + 2 * N))
+    ws = np.zeros(Ls + 2 * N)
+    for t in range(T):
+        s = t * Hs - N // 2 + N
+        ys[:, s:s + N] += y[:, t]
+        ws[s:s + N] += w * w
+    ys, ws = ys[:, N:N + Ls], ws[N:N + Ls]
+    ys = np.where(ws > 1e-6, ys / np.maximum(ws, 1e-6), 0.0)
+    fc = 0.475 / max(r, 1.0)
+    W = 8.0 / (2.0 * fc)
+    out = np.zeros((B, L))
+    for n in range(L):
+        p = n * r
+        j = np.arange(int(math.ceil(p - W)), int(math.floor(p + W)) + 1)
+        j = j[(j >= 0) & (j < Ls) & (np.abs(p - j) < W)]
+        d = p - j
+        hk = 2 * fc * np.sinc(2 * fc * d) * 0.5 * (1 + np.cos(np.pi * d / W))
+        out[:, n] = ys[:, j] @ hk
+    return out
+
+
+def style0(x, sr=16000):
+    """PitchShift(semitones=10) (utils/styles_trigger.py:12-15)."""
+    return pitch_shift(x, sr, 10.0)
+
+
+def style3(x, sr=16000):
+    """PitchShift(10) -> Distortion(20) -> Chorus(rate 1, depth 5, centre 8 ms, mix 0.5)
+    (utils/styles_trigger.py:28-34); the chorus delays its own input, the distorted shifted clip."""
+    y = np.tanh(pitch_shift(x, sr, 10.0) * db_to_gain(20.0))
+    return chorus(y, sr, 1.0, 5.0, 8.0, 0.0, 0.5)

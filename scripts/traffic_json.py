@@ -60,12 +60,19 @@ PHASE_KERNELS = {
 STEP_START = "stft_mel_fast_kernel<"
 
 
+# the sources every bench-step kernel is compiled from (the feature stage, the train step, the fused
+# head included by smallcnn.hip, the shared headers); effects / resample / DABA / the C-ABI glue run
+# no kernel of the bench step, so editing them does not invalidate a traffic measurement
+BENCH_SOURCES = ("mfcc.hip", "smallcnn.hip", "fc_head.inc", "abd_common.h", "prof.h", "prof.cpp")
+
+
 def csrc_sha1(root=HERE):
-    """sha1 over libabd's sources (name + bytes, sorted): identifies the code a measurement belongs to."""
+    """sha1 over the bench step's libabd sources (name + bytes, sorted): identifies the code a
+    measurement belongs to."""
     h = hashlib.sha1()
     d = os.path.join(root, "audio-backdoor-attack_amd", "csrc")
     for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".cpp", ".h")):
+        if f in BENCH_SOURCES:
             h.update(f.encode())
             h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()

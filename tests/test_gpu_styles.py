@@ -65,16 +65,60 @@ def test_fast_path_matches_generic_chain(dev, monkeypatch):
         assert float((f - s).abs().max()) <= 1e-6 * float(s.abs().max())
 
 
-def test_gathered_rows_and_unsupported_styles(dev):
+def test_gathered_rows_and_unsupported_chains(dev):
     x = torch.tensor(clips(8, 16000, seed=2), device=dev)
-    board = T.get_boards()[5]
-    rows = torch.tensor([5, 0, 5], dtype=torch.int32, device=dev)
-    y = board.apply_device(x, 16000, rows=rows)
-    full = board.apply_device(x, 16000)
-    assert torch.equal(y[0], full[5]) and torch.equal(y[1], full[0]) and torch.equal(y[2], full[5])
-    for s in (0, 3):   # PitchShift (Rubber Band)
-        with pytest.raises(AbdError, match="not accelerated"):
-            T.poison_style(x[:1].cpu().numpy(), T.get_boards()[s])
+    for board in (T.get_boards()[5], T.get_boards()[3]):
+        rows = torch.tensor([5, 0, 5], dtype=torch.int32, device=dev)
+        y = board.apply_device(x, 16000, rows=rows)
+        full = board.apply_device(x, 16000)
+        assert torch.equal(y[0], full[5]) and torch.equal(y[1], full[0]) and torch.equal(y[2], full[5])
+    for bad in (T.Pedalboard([T.Gain(3), T.PitchShift(5)]),                 # PitchShift opens a board only
+                T.Pedalboard([T.LadderFilter(), T.Chorus()])):               # a stateful effect before Chorus
+        with pytest.raises(AbdError):
+            bad.apply_device(x, 16000)
+
+
+def pitch_clips(n, L, sr, seed):
+    """tones + a noise floor (no exact silence: the phase vocoder's phases of vanishing bins are
+    rounding noise in any precision, and they persist into later frames)."""
+    r = np.random.default_rng(seed)
+    t = np.arange(L) / sr
+    x = sum(a * np.sin(2 * np.pi * f * t + ph) for a, f, ph in
+            zip(r.uniform(0.05, 0.3, (3, n, 1)), r.uniform(80, 0.2 * sr, (3, n, 1)), r.uniform(0, 6, (3, n, 1))))
+    x = x + r.normal(0, 0.02, (n, L))
+    return np.clip(x, -1, 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("sr,L,semi", [(16000, 16000, 10.0), (16000, 5001, -7.0), (44100, 22050, 10.0)])
+def test_pitch_shift_matches_oracle(dev, sr, L, semi):
+    """The pitch stage (phase vocoder + resample, N = 1024 below 32 kHz, 2048 above) vs
+    oracle/effects.py's float64 restatement: every sample within 1e-4 of the output's max.
+    (Rubber Band itself is absent: parity unpinned against pedalboard.)"""
+    x = pitch_clips(4, L, sr, seed=int(sr + L))
+    y = T.Pedalboard([T.PitchShift(semi)]).apply_device(torch.tensor(x, device=dev), sr).cpu().numpy()
+    ref = oe.pitch_shift(x, sr, semi)
+    assert y.shape == x.shape
+    assert rel(y, ref) < 1e-4, rel(y, ref)
+
+
+def test_pitch_styles_0_and_3(dev):
+    """styles 0 and 3 end to end (utils/styles_trigger.py:12-34): the tone moves by 10 semitones,
+    style 3's Distortion -> Chorus chain runs on the shifted clip (Chorus delays ITS input)."""
+    sr, L = 16000, 16000
+    x = pitch_clips(3, L, sr, seed=7)
+    t = np.arange(L) / sr
+    x[0] = (0.3 * np.sin(2 * np.pi * 440.0 * t) + 0.01 * np.random.default_rng(1).normal(size=L)).astype(np.float32)
+    y0 = T.poison_style(x[:, None], T.get_boards()[0], sr)[:, 0]
+    assert rel(y0, oe.style0(x)) < 1e-4
+    seg = y0[0, 2000:14000] * np.hanning(12000)
+    peak = np.argmax(np.abs(np.fft.rfft(seg))) * sr / 12000
+    assert abs(peak - 440.0 * 2 ** (10 / 12)) < 2.0, peak
+    y3 = T.poison_style(x[:, None], T.get_boards()[3], sr)[:, 0]
+    # the chain alone on the device's own shifted clips (tanh x 10 drive amplifies the stage's
+    # 1e-5-level differences), then the whole board against the oracle
+    chain = oe.chorus(np.tanh(y0.astype(np.float64) * oe.db_to_gain(20.0)), sr, 1.0, 5.0, 8.0, 0.0, 0.5)
+    assert rel(y3, chain) < 1e-5, rel(y3, chain)
+    assert rel(y3, oe.style3(x)) < 1e-3, rel(y3, oe.style3(x))
 
 
 @pytest.mark.parametrize("style", [2, 4])

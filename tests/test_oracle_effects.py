@@ -51,3 +51,34 @@ def test_reverb_dry_only_and_decaying_tail():
     y = oe.reverb(x, 16000, room_size=0.6)
     e1, e2 = (y[0, 500:2500] ** 2).sum(), (y[0, 4000:6000] ** 2).sum()
     assert e1 > 0 and 0 < e2 < e1          # a finite, decaying tail after the impulse
+
+
+def test_pitch_shift_moves_a_tone_and_keeps_length():
+    sr, L = 16000, 16000
+    t = np.arange(L) / sr
+    x = (0.3 * np.sin(2 * np.pi * 440.0 * t))[None]
+    for semi in (10.0, -5.0):
+        y = oe.pitch_shift(x, sr, semi)
+        assert y.shape == x.shape
+        seg = y[0, 2000:14000] * np.hanning(12000)
+        peak = np.argmax(np.abs(np.fft.rfft(seg))) * sr / 12000
+        assert abs(peak - 440.0 * 2 ** (semi / 12)) < 2.0, (semi, peak)
+        assert 0.7 < y[0, 2000:14000].std() / x[0, 2000:14000].std() < 1.1
+
+
+def test_pitch_shift_zero_semitones_reconstructs_band():
+    """r = 1: analysis = synthesis hops, the phase vocoder reproduces the frames exactly, and the
+    resampler is a 0.95-band lowpass: in-band content comes back to ~1e-5."""
+    sr, L = 16000, 8000
+    t = np.arange(L) / sr
+    x = (0.2 * np.sin(2 * np.pi * 300.0 * t) + 0.1 * np.sin(2 * np.pi * 2500.0 * t + 1.0))[None]
+    y = oe.pitch_shift(x, sr, 0.0)
+    assert np.abs(y - x)[0, 200:-200].max() < 1e-4
+    r, N, Hs = oe.pitch_params(44100, 3.0)
+    assert N == 2048 and Hs == 512 and abs(r - 2 ** 0.25) < 1e-12
+
+
+def test_style3_chorus_reads_its_own_input():
+    x = np.random.default_rng(5).normal(0, 0.1, (2, 4000))
+    y = oe.style3(x)
+    assert y.shape == x.shape and np.abs(y).max() <= 1.0 + 1e-12
