@@ -1983,7 +1983,11 @@ template <> struct Terms<1> {
 // <2, 32, 1> (48 KB, smaller tiles for their 150-180 k rows).
 // PA: the A source comes pre-split (NTArgs::srcs, store_planes4): NP 16-B plane loads per fragment
 // replace the two fp32 loads and the in-register split.
-template <int EPI, int NJ, int CS, int MI, int PDW, int WPB, int NP = 3, bool PA = false>
+// KO: K-step order.  false: tap-major (step ks = tap * CS/16 + channel group);  true: channel-
+// group-major (ks = group * 4 + tap), so the four taps of one 16-channel group -- the same source
+// rows shifted by (0,0) (0,1) (1,0) (1,1) -- are consecutive steps and re-read L1-resident lines
+// (a wave's working set per group: ~46 rows x 64 B instead of ~46 rows x 256 B per tap).
+template <int EPI, int NJ, int CS, int MI, int PDW, int WPB, int NP = 3, bool PA = false, bool KO = false>
 __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   constexpr int N = 32 * NJ, K = 4 * CS, LD = K + 8, KS = K / 16, TR = 32 * MI;
   static_assert(KS % PDW == 0, "a tile's K steps must be a whole number of ring turns");
@@ -2074,7 +2078,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
     constexpr int NR = PA ? NP : 2;  // 16-B registers per A fragment: fp32 lo/hi, or the planes
     uint4 raw[PDW][MI][NR];  // [slot][i][.]: slot ks % PDW, refilled with the step PDW later once used
     auto load = [&](const RowInfo& li, int ks, uint4 (&r)[MI][NR]) {
-      const int t = ks / (CS / 16), c16 = ks % (CS / 16);
+      const int t = KO ? ks % 4 : ks / (CS / 16), c16 = KO ? ks / 4 : ks % (CS / 16);
       const uint32_t tofs = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * CS + c16 * 16) * EB);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -2090,7 +2094,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
     // bvs[ks & 1] while the reads for step ks + 1 are in flight (LDS latency off the MFMA path)
     bf16x8 bvs[2][NJ][NP];
     auto load_b = [&](int ks, bf16x8 (&bv)[NJ][NP]) {
-      const int kb = ks * 16 + kq;  // k = tap * CS + channel, 16 per step
+      const int kb = (KO ? (ks % 4) * CS + (ks / 4) * 16 : ks * 16) + kq;  // k = tap * CS + channel
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -3941,26 +3945,46 @@ bool ws_on() {
 // blocks of a launch: one 8-wave block per CU.  conv3 (48 KB of weights, 132-190 VGPRs) also fits
 // only one 8-wave block per CU, so ABD_WS3_MULT=2 runs its second block per CU as a second round
 // (measured: conv3 fwd 0.037 -> 0.033 ms, dgrad 0.031 -> 0.026 ms with one)
-int ws_blocks(int N, int Cs) {
+// Small problems (FlowMur's 32 x 13 input: conv2 has 23 k rows at B = 256) get no more blocks than
+// give every wave one 32-row tile: each block stages the whole weight operand into its LDS, so the
+// full grid would stage it 256 times for ~11 rows per wave (ABD_WS_MIN_TILES: tiles per wave)
+int ws_blocks(int N, int Cs, int64_t M) {
   static const int m3 = std::max(1, env_int("ABD_WS3_MULT", 1));
-  return (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
+  static const int mt = std::max(0, env_int("ABD_WS_MIN_TILES", 1));
+  const int full = (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
+  if (mt == 0) return full;
+  const int64_t need = (M + 8 * 32 * (int64_t)mt - 1) / (8 * 32 * (int64_t)mt);  // 8-wave blocks
+  return (int)std::max<int64_t>(1, std::min<int64_t>(full, need));
 }
 template <int EPI, int NP = 3, bool PA = false>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
   if (PA && (a.srcs == nullptr || a.N != 64 || a.Cs != 64)) return -1;
-  const int nb = ws_blocks(a.N, a.Cs);
+  const int nb = ws_blocks(a.N, a.Cs, a.M);
   if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
   if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
   static const int cfg = env_int("ABD_WS_CFG", 2);  // conv2 tile / ring / waves-per-block (A/B knob)
-  if (PA) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 64 && (cfg == 2 || NP == 1)) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (NP == 3 && a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 32 && a.Cs == 64) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 32) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else {
+  // K-step order (see the kernel): channel-group-major for the forward (conv2 0.147 -> 0.141 ms),
+  // tap-major for the data gradient (0.133 vs 0.136 ms channel-major); ABD_WS_KORD 0 / 1 / 2 =
+  // tap-major everywhere / forward only / both
+  static const int kord = env_int("ABD_WS_KORD", 1);
+  const bool ko = kord == 2 || (kord == 1 && EPI == EPI_CONV);
+  if (PA) {
+    if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+  } else if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
+  else if (a.N == 64 && a.Cs == 64 && (cfg == 2 || NP == 1)) {
+    if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, false, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  } else if (NP == 3 && a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  else if (a.N == 32 && a.Cs == 64) {
+    if (ko) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP, false, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  } else if (a.N == 64 && a.Cs == 32) {
+    if (ko) conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8, NP, false, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else conv_ws_split_kernel<EPI, 2, 32, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  } else {
     if (phase >= 0) abd::prof_end(phase, s);
     return -1;
   }
@@ -4216,7 +4240,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
     const bool ws = (sp || bf) && ws_on();  // bf16: the same weight-stationary kernel on one plane
-    a.nblk = ws ? ws_blocks(64, 64)
+    a.nblk = ws ? ws_blocks(64, 64, a.M)
              : bf ? (a.M + kBM - 1) / kBM
              : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
              : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
@@ -4270,7 +4294,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
     const bool ws3 = (sp3 || bf3) && ws_on();
-    a.nblk = ws3 ? ws_blocks(32, 64) : (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
+    a.nblk = ws3 ? ws_blocks(32, 64, a.M) : (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     if (ws3   ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
                      : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))

@@ -254,8 +254,16 @@ def _princarg(x):
     return x - 2 * np.pi * np.rint(x / (2 * np.pi))
 
 
-def pitch_shift(x, sr, semitones=10.0):
-    """(B, L) -> (B, L) float64."""
+def pitch_shift(x, sr, semitones=10.0, replay=None, tie_tol=2e-3):
+    """(B, L) -> (B, L) float64.
+
+    Decision replay (tests): the wrap of dphi -- princarg's choice of the nearest multiple of 2 pi
+    -- is a discrete decision that r's non-integer multiplier turns into a 2 pi (r - 1) jump of
+    phi_s; at dphi within rounding of +-pi ANY two precisions may choose differently, and the
+    vocoder carries the difference into every later frame of that bin.  ``replay`` = the device's
+    synthesized spectra Y (B, T, K complex): where the device's phase matches a neighbouring wrap,
+    the oracle takes it, after checking the decision was a genuine near-tie (|u - rint(u)| within
+    ``tie_tol`` of 1/2, u = dphi / 2 pi before wrapping).  Returns (out, replayed decisions)."""
     x = np.asarray(x, dtype=np.float64)
     B, L = x.shape
     r, N, Hs = pitch_params(sr, semitones)
@@ -272,10 +280,28 @@ def pitch_shift(x, sr, semitones=10.0):
     k = np.arange(K)
     ps = np.empty_like(pha)
     ps[:, 0] = pha[:, 0]
+    nrep = 0
     for t in range(1, T):
         h = int(ia[t] - ia[t - 1])
-        dphi = _princarg(pha[:, t] - pha[:, t - 1] - 2 * np.pi * ((k * h) % N) / N)
-        ps[:, t] = _princarg(ps[:, t - 1] + 2 * np.pi * ((k * Hs) % N) / N + (Hs / h) * dphi)
+        raw = pha[:, t] - pha[:, t - 1] - 2 * np.pi * ((k * h) % N) / N
+        dphi = _princarg(raw)
+        base = ps[:, t - 1] + 2 * np.pi * ((k * Hs) % N) / N
+        ps[:, t] = _princarg(base + (Hs / h) * dphi)
+        if replay is not None:
+            dev = np.angle(replay[:, t])
+            live = np.abs(replay[:, t]) > 0
+            best = np.abs(np.angle(np.exp(1j * (ps[:, t] - dev))))
+            for sh in (-1.0, 1.0):
+                cand = _princarg(base + (Hs / h) * (dphi + sh * 2 * np.pi))
+                dist = np.abs(np.angle(np.exp(1j * (cand - dev))))
+                take = live & (dist < best) & (dist < 0.1)
+                if take.any():
+                    u = raw[take] / (2 * np.pi)
+                    assert np.all(np.abs(np.abs(u - np.rint(u)) - 0.5) < tie_tol), \
+                        f"frame {t}: a wrap decision that is not a near-tie ({np.abs(u - np.rint(u)).min()})"
+                    ps[:, t][take] = cand[take]
+                    best = np.where(take, dist, best)
+                    nrep += int(take.sum())
     Y = mag * np.exp(1j * ps)
     y = np.fft.irfft(Y, n=N, axis=2) * w                                # (B, T, N)
     ys = np.zeros((B, Ls + 2 * N))
@@ -296,7 +322,7 @@ def pitch_shift(x, sr, semitones=10.0):
         d = p - j
         hk = 2 * fc * np.sinc(2 * fc * d) * 0.5 * (1 + np.cos(np.pi * d / W))
         out[:, n] = ys[:, j] @ hk
-    return out
+    return (out, nrep) if replay is not None else out
 
 
 def style0(x, sr=16000):
@@ -304,8 +330,9 @@ def style0(x, sr=16000):
     return pitch_shift(x, sr, 10.0)
 
 
-def style3(x, sr=16000):
+def style3(x, sr=16000, shifted=None):
     """PitchShift(10) -> Distortion(20) -> Chorus(rate 1, depth 5, centre 8 ms, mix 0.5)
-    (utils/styles_trigger.py:28-34); the chorus delays its own input, the distorted shifted clip."""
-    y = np.tanh(pitch_shift(x, sr, 10.0) * db_to_gain(20.0))
+    (utils/styles_trigger.py:28-34); the chorus delays its own input, the distorted shifted clip.
+    ``shifted``: the PitchShift output to continue from (decision-replayed runs)."""
+    y = np.tanh((pitch_shift(x, sr, 10.0) if shifted is None else shifted) * db_to_gain(20.0))
     return chorus(y, sr, 1.0, 5.0, 8.0, 0.0, 0.5)
