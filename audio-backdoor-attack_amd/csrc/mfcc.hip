@@ -37,6 +37,19 @@ constexpr int kTT = 8;                     // frames per db_dct block
 constexpr int kQueues = 8;                 // fast-kernel item queues (one per XCD)
 constexpr int kQueueStride = 64;           // unsigned words between queue counters (256 B)
 
+// ABD_STFT_ABLATE (diagnostic builds only: -DABD_STFT_ABLATE_BUILD): the fast kernel's ablation
+// switches; compiled out otherwise (their wave-uniform tests cost SGPRs the kernel spills)
+#ifdef ABD_STFT_ABLATE_BUILD
+constexpr bool kAblate = true;
+#else
+constexpr bool kAblate = false;
+#endif
+#ifdef ABD_GATHER_SCALAR
+constexpr bool kGatherV4 = false;  // A/B build: the per-element gather everywhere
+#else
+constexpr bool kGatherV4 = true;
+#endif
+
 struct MfccDev {
   int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
   int ablate;  // diagnostics only (ABD_STFT_ABLATE): 1 skip sample loads, 2 skip FFTs, 4 skip mel
@@ -57,7 +70,10 @@ struct MfccDev {
   int dct_tiles;           // ceil(n_mfcc / 16) when the MFMA DCT applies (n_mels % 16 == 0, n_mfcc <= 48), else 0
   // fast (specialised) kernel tables
   const float2* ftw;      // [W_{R0 R1}^e] ++ [W_M^k], e, k < R0 R1
-  const float2* ftw2;     // fast forward kernel: [k][r] tables W_{R0 R1}^{k r} (k < R0, r < R1) ++
+  const float4* chirp_out2;  // Bluestein fast kernel: (chirp_out[k], chirp_out[k ? N - k : 0]), k <= N/2
+  const float4* ftw4;     // fast kernel pass 2: [p][k] (W_{R0 R1}^{k (1+2p)}, W_{R0 R1}^{k (2+2p)}), p < R1/2
+  const float4* vhat4;    // Bluestein fast kernel: [p][j] (vhat[j + 2p M/R0], vhat[j + (2p+1) M/R0]), p < R0/2
+  const float2* ftw2;     // fast forward kernel: [r][k] tables W_{R0 R1}^{k r} (k < R0, r < R1) ++
                           // W_M^{k r} (k < R0 R1, r < R2): every twiddle load is base + immediate
   const int4* mel2_meta;  // per half-filter slot 2m+h: (first bin, count, weight offset, 0)
   const float* mel2_w;    // compact slot weights
@@ -679,6 +695,10 @@ __device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
 }
 // value the compiler must treat as defined without materialising it (skip paths of the
 // wave-uniform pass guards: otherwise the backend zero-fills every register of the butterfly)
+// An opaque unspecified value.  (freeze(poison) -- __builtin_nondeterministic_value -- removes the
+// s_nop the hazard recognizer puts before each empty asm, but lets the compiler turn the
+// wave-uniform skip branches into selects: the idle waves of a partial pass then computed their
+// clamped butterflies, +23 % VALU instructions in the Bluestein kernel, measured.)
 __device__ __forceinline__ f2v undef_f2v() {
   f2v v;
   asm volatile("" : "=v"(v));
@@ -904,7 +924,7 @@ __device__ __forceinline__ void spass(float2* __restrict__ bufs, const float2* _
         } else if constexpr (TWK == 2) {
           if (r > 0) a = cmul_rt(a, w[r]);
         } else if constexpr (TWK == 3) {
-          if (r > 0) a = cmul_rt(a, tw[k * R + r]);
+          if (r > 0) a = cmul_rt(a, tw[r * NS + k]);
         }
         v[rd][r] = a;
       }
@@ -957,13 +977,32 @@ __device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const fl
 // registers are free there: the previous pass's values are already stored), so their latency
 // overlaps the barrier wait instead of stalling the DFT; then LDS reads -> DFT -> barrier ->
 // writes.  No trailing barrier: the next pass (or the caller) opens with one.
-//   TWK 0: none;  2: W_M^k base (ftw2 pass-3 table column r = 1) + tw_powers;  3: [k][r] table
+//   TWK 0: none;  2: W_M^k base (ftw2 pass-3 table column r = 1) + tw_powers;  3: [r][k] table;
+//        4: [pair][k] float4 table (MfccDev::ftw4: rows 1 + 2p and 2 + 2p in one 16-B load)
+//   V4 (with VMUL): Bluestein's vhat as [pair][j] float4 (MfccDev::vhat4: rows 2p, 2p + 1)
 //   PF: rows r < PF are prefetched, the rest loaded after the barrier (VGPR budget of 8 blocks/CU)
+// The pair tables halve the pass's vector-memory instructions: the kernel's vector-memory data
+// path (TD) was ~90 % busy, its wave-load count -- not bytes or L1 misses -- the limit.
 constexpr int kPrefetchRows = 8;
-template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R, int RS = R, int PF = kPrefetchRows>
+template <int R, int PF, int ZT, int LO>
+__device__ __forceinline__ void pair_rows(f2v* pre, const float4* __restrict__ t4, int idx, int stride, bool after) {
+  // rows LO + 2p and LO + 1 + 2p from t4[p * stride + idx]; `after`: only pairs whose first row is
+  // past the prefetch budget, else only those within it
+#pragma unroll
+  for (int p = 0; p < R / 2; ++p) {
+    const int r0 = LO + 2 * p;
+    if (r0 >= R || r0 >= ZT || (after ? r0 < PF : r0 >= PF)) continue;
+    const float4 q = t4[p * stride + idx];
+    pre[r0] = f2v{q.x, q.y};
+    if (r0 + 1 < R) pre[r0 + 1] = f2v{q.z, q.w};
+  }
+}
+template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R, int RS = R, int PF = kPrefetchRows,
+          bool V4 = false>
 __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2* __restrict__ tws,
-                                         const float2* __restrict__ vhats) {
+                                         const float2* __restrict__ vhats, const float4* __restrict__ t4 = nullptr) {
   static_assert(!(VMUL && TWK != 0), "vhat product and twiddles never share a pass");
+  static_assert(!V4 || VMUL, "V4 is the vhat pair table");
   constexpr int MR = M / R;
   constexpr int NB = PP * MR;
   constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
@@ -981,11 +1020,13 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
     if (ROUNDS * kThreads == NB || __builtin_amdgcn_readfirstlane(tid & ~63) + rd * kThreads < NB) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if constexpr (VMUL) pre[rd][r] = (r < ZT && r < PF) ? vhat[j + r * MR] : undef_f2v();
-        else if constexpr (TWK == 3) pre[rd][r] = (r > 0 && r < PF) ? tw[k * R + r] : undef_f2v();
-        else if constexpr (TWK == 2) pre[rd][r] = (r == 1) ? tw[k * R + 1] : undef_f2v();
+        if constexpr (VMUL && !V4) pre[rd][r] = (r < ZT && r < PF) ? vhat[j + r * MR] : undef_f2v();
+        else if constexpr (TWK == 3) pre[rd][r] = (r > 0 && r < PF) ? tw[r * NS + k] : undef_f2v();
+        else if constexpr (TWK == 2) pre[rd][r] = (r == 1) ? tw[NS + k] : undef_f2v();
         else pre[rd][r] = undef_f2v();
       }
+      if constexpr (TWK == 4) pair_rows<R, PF, R, 1>(pre[rd], t4, k, NS, false);
+      if constexpr (V4) pair_rows<R, PF, ZT, 0>(pre[rd], t4, j, MR, false);
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) pre[rd][r] = undef_f2v();
@@ -1005,12 +1046,14 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
       if constexpr (TWK == 2) tw_powers<R>(pre[rd][1], pre[rd]);
 #pragma unroll
       for (int r = PF; r < R; ++r) {  // rows past the prefetch budget
-        if constexpr (VMUL) {
+        if constexpr (VMUL && !V4) {
           if (r < ZT) pre[rd][r] = vhat[j + r * MR];
         } else if constexpr (TWK == 3) {
-          pre[rd][r] = tw[k * R + r];
+          pre[rd][r] = tw[r * NS + k];
         }
       }
+      if constexpr (TWK == 4) pair_rows<R, PF, R, 1>(pre[rd], t4, k, NS, true);
+      if constexpr (V4) pair_rows<R, PF, ZT, 0>(pre[rd], t4, j, MR, true);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (r >= ZT) {
@@ -1056,13 +1099,24 @@ constexpr int kTw3 = 3;
 #else
 constexpr int kTw3 = 2;
 #endif
+// pass 2: 4 = the [pair][k] float4 table (default); 3 = the [r][k] table; 2 = one W_{R0 R1}^k load
+// (ftw2 row 1) + tw_powers (A/B builds: -DABD_TW2=3 / 2).  The powers measured as fast as the pair
+// table (0.239 vs 0.240 ms) but their ~6-rounding-deep factors moved a FlowMur top_db clamp
+// decision: the trigger gradient left the autograd golden by 8.5e-3 (tests/test_gpu_flowmur.py)
+#ifdef ABD_TW2
+constexpr int kTw2 = ABD_TW2;
+#else
+constexpr int kTw2 = 4;
+#endif
 template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M, int NO = M>
-__device__ __forceinline__ void fft_plan_pf(float2* buf, const float2* tw, const float2* vhat) {
+__device__ __forceinline__ void fft_plan_pf(float2* buf, const float2* tw, const float2* vhat, const float4* tw4,
+                                            const float4* vhat4) {
   static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
   static_assert(NO == M || R2 > 1, "output pruning needs a third pass");
   constexpr int MR0 = M / R0;
-  spass_pf<M, R0, 1, PP, 0, VMUL, (NZ + MR0 - 1) / MR0>(buf, nullptr, vhat);
-  spass_pf<M, R1, R0, PP, 3, false>(buf, tw, nullptr);
+  constexpr int ZT0 = (NZ + MR0 - 1) / MR0;
+  spass_pf<M, R0, 1, PP, 0, VMUL, ZT0, R0, kPrefetchRows, VMUL>(buf, nullptr, vhat, vhat4);
+  spass_pf<M, R1, R0, PP, kTw2, false>(buf, tw, nullptr, tw4);
   if constexpr (R2 > 1)
     spass_pf<M, R2, R0 * R1, PP, kTw3, false, R2, (NO + R0 * R1 - 1) / (R0 * R1)>(buf, tw + R0 * R1, nullptr);
 }
@@ -1121,7 +1175,7 @@ __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const floa
       ok[q] = (g0 + q < ITERS) && (idx < TOT) && (n < NN) && (PP == 1 || INTERIOR || f < np);
       const int t0 = 2 * (p0 + f);
       const int i0 = t0 * hop + n - p.pad, i1 = i0 + hop;
-      if (p.ablate & 1) {
+      if (kAblate && (p.ablate & 1)) {
         a[q] = (float)n;
         b[q] = (float)t0;
       } else if constexpr (INTERIOR) {
@@ -1175,12 +1229,86 @@ __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const floa
   }
 }
 
+// Interior Bluestein items (one frame pair, every sample inside the signal) with no injection or
+// the additive trigger: each thread takes 4 consecutive elements n..n+3, so a frame's samples come
+// as one (dword-aligned) 16-B load, the chirp as two, the trigger as one -- a quarter of the
+// per-element path's vector-memory instructions, which bound the kernel (TD busy ~85-90 %).
+// Same arithmetic per element as load_frames / fsample.
+template <int M, int NN, int MODE, int NZW>
+__device__ __forceinline__ void load_frames_v4(float2* __restrict__ buf, const float* __restrict__ x, const MfccDev& p,
+                                               const InjDev& inj, int p0) {
+  static_assert(MODE == ABD_INJECT_NONE || MODE == ABD_INJECT_ADD, "vector gather: no / additive injection");
+  static_assert(NZW % 4 == 0, "element groups of 4");
+  constexpr int GROUPS = NZW / 4;
+  constexpr int ITERS = (GROUPS + kThreads - 1) / kThreads;
+  const int hop = p.hop;
+  const int base = 2 * p0 * hop - p.pad;  // sample of frame a's element 0
+  const int tl = (int)inj.trig_len;
+  const float4* ci4 = reinterpret_cast<const float4*>(p.chirp_in);
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int gi = ltid() + it * kThreads;
+    if (ITERS * kThreads != GROUPS && gi >= GROUPS) break;
+    const int n = 4 * gi;
+    float a[4], b[4];
+    float2 c[4];
+    if (n + 3 < NN) {
+      const int s0 = base + n, s1 = s0 + hop;
+      float4 va, vb;
+      __builtin_memcpy(&va, x + s0, 16);
+      __builtin_memcpy(&vb, x + s1, 16);
+      const float4 c01 = ci4[2 * gi], c23 = ci4[2 * gi + 1];
+      a[0] = va.x; a[1] = va.y; a[2] = va.z; a[3] = va.w;
+      b[0] = vb.x; b[1] = vb.y; b[2] = vb.z; b[3] = vb.w;
+      c[0] = make_float2(c01.x, c01.y); c[1] = make_float2(c01.z, c01.w);
+      c[2] = make_float2(c23.x, c23.y); c[3] = make_float2(c23.z, c23.w);
+      if constexpr (MODE == ABD_INJECT_ADD) {
+        // v + t for samples s < tl (fsample): whole groups by one 16-B trigger load each
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int sb = h ? s1 : s0;
+          float* v = h ? b : a;
+          if (sb + 3 < tl) {
+            float4 tv;
+            __builtin_memcpy(&tv, inj.trig + sb, 16);
+            v[0] += tv.x; v[1] += tv.y; v[2] += tv.z; v[3] += tv.w;
+          } else if (sb < tl) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (sb + e < tl) v[e] += inj.trig[sb + e];
+          }
+        }
+      }
+    } else {  // the group straddling NN: per element, zero past the frame
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = n + e < NN;
+        const int s0 = base + min(n + e, NN - 1);
+        a[e] = ok ? fsample<MODE>(x, inj, s0, 0, 0.0f) : 0.0f;
+        b[e] = ok ? fsample<MODE>(x, inj, s0 + hop, 0, 0.0f) : 0.0f;
+        c[e] = p.chirp_in[min(n + e, NN - 1)];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f2v zz = cmul_rt(f2v{a[e], b[e]}, f2v{c[e].x, c[e].y});
+      buf[pidx(n + e)] = (n + e < NN) ? make_float2(zz.x, zz.y) : make_float2(0.0f, 0.0f);
+    }
+  }
+}
+
 template <int M, int NN, int PP, bool BLUE, int MODE, int NZW = M>
 __device__ __forceinline__ void load_item(float2* buf, const float* x, const MfccDev& p, const InjDev& inj, int pos,
                                           float rs, int p0, int np) {
   const int first = 2 * p0 * p.hop - p.pad;
   const int last_t = 2 * (p0 + PP) - 1;
   const bool interior = np == PP && first >= 0 && last_t < p.T && last_t * p.hop - p.pad + NN <= (int)p.L;
+  if constexpr (BLUE && PP == 1 && (MODE == ABD_INJECT_NONE || MODE == ABD_INJECT_ADD) && NZW % 4 == 0) {
+    if (interior && kGatherV4) {
+      load_frames_v4<M, NN, MODE, NZW>(buf, x, p, inj, p0);
+      return;
+    }
+  }
   if (interior) load_frames<M, NN, PP, BLUE, MODE, true, NZW>(buf, x, p, inj, pos, rs, p0, np);
   else load_frames<M, NN, PP, BLUE, MODE, false, NZW>(buf, x, p, inj, pos, rs, p0, np);
 }
@@ -1215,15 +1343,14 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
   static_assert(POFF + NF + kMelHP <= M + M / 16, "power array must fit the FFT buffer");
   f2v* buf = reinterpret_cast<f2v*>(bufs);
   f2v* pw = buf + POFF;
-  const f2v* co = reinterpret_cast<const f2v*>(p.chirp_out);
   constexpr int PR = (NF + kMelHP + kThreads - 1) / kThreads;
   f2v cq[PR][2];  // output chirps, loaded ahead of the barrier that publishes the last FFT pass
 #pragma unroll
   for (int rd = 0; rd < PR; ++rd) {
     const int k = min(ltid() + rd * kThreads, NF - 1);
-    const int kn = (k == 0) ? 0 : NN - k;
-    cq[rd][0] = co[k];
-    cq[rd][1] = co[kn];
+    const float4 c2 = p.chirp_out2[k];  // (w[k] / M, w[N - k] / M): one 16-B load per bin
+    cq[rd][0] = f2v{c2.x, c2.y};
+    cq[rd][1] = f2v{c2.z, c2.w};
   }
   __syncthreads();
 #pragma unroll
@@ -1247,11 +1374,11 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
   __syncthreads();
   const int sl = ltid();
   const int start = p.mel2_meta[sl].x;
-  const float4* wq = reinterpret_cast<const float4*>(p.mel3_w) + sl * (kMelHP / 4);
+  const float4* wq = reinterpret_cast<const float4*>(p.mel3_w) + sl;  // [q][slot], 2 n_mels == kThreads slots
   float w[kMelHP];
 #pragma unroll
   for (int q = 0; q < kMelHP / 4; ++q) {
-    const float4 v = wq[q];
+    const float4 v = wq[q * kThreads];
     w[4 * q] = v.x;
     w[4 * q + 1] = v.y;
     w[4 * q + 2] = v.z;
@@ -1274,8 +1401,10 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
   return lmax;
 }
 
-template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
-__global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
+// NBLK: blocks per CU the Bluestein build is register-budgeted for (8: 64 VGPRs and <= 80 SGPRs, the
+// compiler spills SGPRs into VGPR lanes; 7: 72 VGPRs / 96 SGPRs, no spills, one block fewer)
+template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE, int NBLK = kBlueBlocks>
+__global__ void __launch_bounds__(kThreads, BLUE ? NBLK : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
                                                                  int64_t row_stride,
                                                                  const int32_t* __restrict__ rows, int64_t batch,
                                                                  InjDev inj, const float* __restrict__ rowscale,
@@ -1352,19 +1481,19 @@ __global__ void __launch_bounds__(kThreads, BLUE ? kBlueBlocks : 1) stft_mel_fas
       default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
     }
     // no barrier here: the first pass opens with the one that publishes the loaded frames
-    if (!(p.ablate & 2)) {
-      fft_plan_pf<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr);
-      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PP, true, M, NN>(buf, tw, p.vhat);
+    if (!(kAblate && (p.ablate & 2))) {
+      fft_plan_pf<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr, p.ftw4, nullptr);
+      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PP, true, M, NN>(buf, tw, p.vhat, p.ftw4, p.vhat4);
     }
     float lmax = -INFINITY;
     if constexpr (BLUE && PP == 1) {
-      if (p.mel3_w != nullptr && !(p.ablate & 4)) {
+      if (p.mel3_w != nullptr && !(kAblate && (p.ablate & 4))) {
         lmax = power_mel_blue<M, NN>(buf, p, ws_db + (int64_t)u * p.T * p.n_mels, 2 * p0);
         goto item_done;
       }
     }
     __syncthreads();  // the last pass's writes (fft_plan_pf leaves no trailing barrier)
-    if (!(p.ablate & 4)) {
+    if (!(kAblate && (p.ablate & 4))) {
       // Power of the two real spectra, written over Z[k] (k <= N/2).  Z[k] is read only by
       // the thread that owns bin k (Z[N-k] with N-k > N/2 is never written), so no barrier
       // is needed between the reads and the in-place writes.
@@ -1717,11 +1846,11 @@ const FastPlan* find_fast(int M, int N, int blue) {
   return nullptr;
 }
 
-template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE>
+template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE, int NBLK = kBlueBlocks>
 int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
                 const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
                 hipStream_t s) {
-  auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE>;
+  auto* kern = &stft_mel_fast_kernel<M, NN, R0, R1, R2, PP, BLUE, NBLK>;
   static_assert(M % 16 == 0, "padded LDS layout needs M % 16 == 0");
   size_t lds = (size_t)(PP * (M + M / 16)) * sizeof(float2);
 #ifdef ABD_MEL_W_LDS
@@ -1762,6 +1891,10 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
 int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
                   const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
                   hipStream_t s) {
+  static const int nblk = getenv("ABD_STFT_BLOCKS") ? atoi(getenv("ABD_STFT_BLOCKS")) : 8;  // A/B knob
+  if (d.M == 2304 && d.N == 1103 && d.bluestein && nblk == 7)
+    return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true, 7>(d, wave, row_stride, rows, batch, ij, rowscale,
+                                                                          ws_db, ws_max, queue, s);
   if (d.M == 2304 && d.N == 1103 && d.bluestein)
     return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
                                                        queue, s);
@@ -2059,9 +2192,12 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   // padded slot weights for the Bluestein fast path (power_mel_blue): one slot per thread
   const bool mel3 = blue && d.fast && 2 * n_mels == kThreads && hmax <= kMelHP;
   std::vector<float> mw3(mel3 ? (size_t)2 * n_mels * kMelHP : 0, 0.0f);
+  // [q][slot] float4 groups: the q-th float4 load of the mel stage is one contiguous 4 KB sweep
+  // across the 256 slots (lanes) instead of 64-B pieces 64 B apart
   if (mel3)
     for (int sl = 0; sl < 2 * n_mels; ++sl)
-      for (int i = 0; i < meta2[sl].y; ++i) mw3[(size_t)sl * kMelHP + i] = mw2[meta2[sl].z + i];
+      for (int i = 0; i < meta2[sl].y; ++i)
+        mw3[(((size_t)(i / 4) * (2 * n_mels) + sl) * 4) + (i % 4)] = mw2[meta2[sl].z + i];
   // fast-kernel twiddles: W_{R0 R1}^e and W_M^k, e, k < R0 R1
   const int r01 = fp ? fp->r0 * fp->r1 : 1;
   std::vector<float2> ftw(2 * (size_t)r01);
@@ -2073,18 +2209,51 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   std::vector<float2> ftw2;
   if (fp) {
     const int r0 = fp->r0, r1 = fp->r1, r2 = M / (r0 * r1);
-    for (int k = 0; k < r0; ++k)
-      for (int r = 0; r < r1; ++r) {
+    // [r][k]: for a fixed row r the lanes of a wave (consecutive butterflies j, k = j mod NS) read
+    // consecutive entries -- one or two cache lines per wave load instead of one line per lane
+    // group at a 96-B stride ([k][r] kept the vector-memory data path 89 % busy)
+    for (int r = 0; r < r1; ++r)
+      for (int k = 0; k < r0; ++k) {
         const double a = -2.0 * M_PI * (double)((k * r) % r01) / r01;
         ftw2.push_back(make_float2((float)cos(a), (float)sin(a)));
       }
-    for (int k = 0; k < r01; ++k)
-      for (int r = 0; r < r2; ++r) {
+    for (int r = 0; r < r2; ++r)
+      for (int k = 0; k < r01; ++k) {
         const double a = -2.0 * M_PI * (double)(((int64_t)k * r) % M) / M;
         ftw2.push_back(make_float2((float)cos(a), (float)sin(a)));
       }
   }
   if (ftw2.empty()) ftw2.push_back(make_float2(1.0f, 0.0f));
+  // pair tables of the fast kernel (spass_pf TWK 4 / V4): two rows per 16-B load
+  std::vector<float4> ftw4, vhat4;
+  if (fp) {
+    const int r0 = fp->r0, r1 = fp->r1;
+    auto w = [&](int k, int r) {
+      const double a = -2.0 * M_PI * (double)((k * r) % r01) / r01;
+      return std::make_pair((float)cos(a), (float)sin(a));
+    };
+    for (int p2 = 0; p2 < r1 / 2; ++p2)
+      for (int k = 0; k < r0; ++k) {
+        const auto a = w(k, 1 + 2 * p2);
+        const auto b = 2 + 2 * p2 < r1 ? w(k, 2 + 2 * p2) : std::make_pair(1.0f, 0.0f);
+        ftw4.push_back(make_float4(a.first, a.second, b.first, b.second));
+      }
+    if (blue) {
+      const int mr0 = M / r0;
+      for (int p2 = 0; p2 < r0 / 2; ++p2)
+        for (int j = 0; j < mr0; ++j) {
+          const float2 a = vhat[j + 2 * p2 * mr0], b = vhat[j + (2 * p2 + 1) * mr0];
+          vhat4.push_back(make_float4(a.x, a.y, b.x, b.y));
+        }
+    }
+  }
+  if (ftw4.empty()) ftw4.push_back(make_float4(1.0f, 0.0f, 1.0f, 0.0f));
+  std::vector<float4> co2((size_t)N / 2 + 1);
+  for (int k = 0; k <= N / 2; ++k) {
+    const float2 a = chirp_out[k], b = chirp_out[k == 0 ? 0 : N - k];
+    co2[k] = make_float4(a.x, a.y, b.x, b.y);
+  }
+  if (vhat4.empty()) vhat4.push_back(make_float4(1.0f, 0.0f, 1.0f, 0.0f));
   std::vector<float> dct((size_t)n_mels * n_mfcc);
   for (int m = 0; m < n_mels; ++m)
     for (int c = 0; c < n_mfcc; ++c) {
@@ -2134,6 +2303,12 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   sz += al(dfrag.size() * sizeof(float4));
   size_t off_ftw2 = sz;
   sz += al(ftw2.size() * sizeof(float2));
+  size_t off_co2 = sz;
+  sz += al(co2.size() * sizeof(float4));
+  size_t off_ftw4 = sz;
+  sz += al(ftw4.size() * sizeof(float4));
+  size_t off_vh4 = sz;
+  sz += al(vhat4.size() * sizeof(float4));
   size_t off_m2 = sz;
   sz += al(meta2.size() * sizeof(int4));
   size_t off_w2 = sz;
@@ -2160,6 +2335,9 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   memcpy(&host[off_ftw], ftw.data(), ftw.size() * sizeof(float2));
   memcpy(&host[off_dfrag], dfrag.data(), dfrag.size() * sizeof(float4));
   memcpy(&host[off_ftw2], ftw2.data(), ftw2.size() * sizeof(float2));
+  memcpy(&host[off_co2], co2.data(), co2.size() * sizeof(float4));
+  memcpy(&host[off_ftw4], ftw4.data(), ftw4.size() * sizeof(float4));
+  memcpy(&host[off_vh4], vhat4.data(), vhat4.size() * sizeof(float4));
   memcpy(&host[off_m2], meta2.data(), meta2.size() * sizeof(int4));
   memcpy(&host[off_w2], mw2.data(), mw2.size() * sizeof(float));
   if (!mw3.empty()) memcpy(&host[off_w3], mw3.data(), mw3.size() * sizeof(float));
@@ -2190,6 +2368,9 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.ftw = reinterpret_cast<const float2*>(b + off_ftw);
   d.dct_frag = reinterpret_cast<const float4*>(b + off_dfrag);
   d.ftw2 = reinterpret_cast<const float2*>(b + off_ftw2);
+  d.ftw4 = reinterpret_cast<const float4*>(b + off_ftw4);
+  d.chirp_out2 = reinterpret_cast<const float4*>(b + off_co2);
+  d.vhat4 = reinterpret_cast<const float4*>(b + off_vh4);
   d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
   d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
   d.mel3_w = mw3.empty() || getenv("ABD_MEL_GENERIC") ? nullptr : reinterpret_cast<const float*>(b + off_w3);
