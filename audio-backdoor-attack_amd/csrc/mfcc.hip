@@ -984,6 +984,10 @@ __device__ __forceinline__ void fft_plan(float2* buf, const float2* tw, const fl
 // The pair tables halve the pass's vector-memory instructions: the kernel's vector-memory data
 // path (TD) was ~90 % busy, its wave-load count -- not bytes or L1 misses -- the limit.
 constexpr int kPrefetchRows = 8;
+// TWK 5: the first L = ceil((R - 1) / 2) rows (rounded up to whole pairs) from the pair table, the
+// rest as one product each -- half the pass-2 twiddle bytes, factors one rounding from the table
+template <int R>
+constexpr int kTw5Rows = (((R - 1 + 1) / 2) + 1) / 2 * 2;
 template <int R, int PF, int ZT, int LO>
 __device__ __forceinline__ void pair_rows(f2v* pre, const float4* __restrict__ t4, int idx, int stride, bool after) {
   // rows LO + 2p and LO + 1 + 2p from t4[p * stride + idx]; `after`: only pairs whose first row is
@@ -1026,6 +1030,7 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
         else pre[rd][r] = undef_f2v();
       }
       if constexpr (TWK == 4) pair_rows<R, PF, R, 1>(pre[rd], t4, k, NS, false);
+      if constexpr (TWK == 5) pair_rows<kTw5Rows<R> + 1, PF, R, 1>(pre[rd], t4, k, NS, false);
       if constexpr (V4) pair_rows<R, PF, ZT, 0>(pre[rd], t4, j, MR, false);
     } else {
 #pragma unroll
@@ -1053,6 +1058,12 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
         }
       }
       if constexpr (TWK == 4) pair_rows<R, PF, R, 1>(pre[rd], t4, k, NS, true);
+      if constexpr (TWK == 5) {
+        pair_rows<kTw5Rows<R> + 1, PF, R, 1>(pre[rd], t4, k, NS, true);
+        // rows past the loaded ones: one product of two table entries each (a + b = r, a, b <= L)
+#pragma unroll
+        for (int r = kTw5Rows<R> + 1; r < R; ++r) pre[rd][r] = cmul_rt(pre[rd][r / 2], pre[rd][r - r / 2]);
+      }
       if constexpr (V4) pair_rows<R, PF, ZT, 0>(pre[rd], t4, j, MR, true);
 #pragma unroll
       for (int r = 0; r < R; ++r) {

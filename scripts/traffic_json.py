@@ -28,14 +28,19 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # phase -> candidate (exact kernel, occurrence within one step); the first candidate present is used
 PHASE_KERNELS = {
-    "stft_mel": [("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
+    "stft_mel": [("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true, 8>", 0),
+                 ("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
     "db_dct": [("db_dct_mfma_kernel<3>", 0)],
     "conv1_stats": [("conv1_stats_fold_kernel", 0), ("conv1_stats_kernel", 0)],
-    "conv2_fwd": [("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false>", 0),
+    "conv2_fwd": [("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false, true>", 0),
+                  ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, true, true>", 0),
+                  ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, true>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, false>", 0)],
     "bn2_pool": [("bn_pool_fwd_kernel", 0)],
-    "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false>", 0),
+    "conv3_fwd": [("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false, true>", 0),
+                  ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 1, false, true>", 0),
+                  ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false>", 0),
                   ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 1, false>", 0)],
     "bn3_pool_dropout": [("bn_pool_fwd_kernel", 1)],
     "head_fwd": [("head_fwd_kernel<4>", 0), ("head_fwd_kernel<8>", 0), ("head_fwd_kernel", 0)],
@@ -49,11 +54,15 @@ PHASE_KERNELS = {
     "bn3_bwd": [("bn_bwd_apply_kernel", -2)],
     "bn2_bwd": [("bn_bwd_apply_kernel", -1)],
     "conv3_wgrad": [("conv_wgrad_trp_kernel<4, 32, 2, 4, 3, false>", 0), ("conv_wgrad_trp_kernel<4, 32, 2, 4, 1, false>", 0)],
-    "conv3_dgrad": [("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 3, false>", 0),
+    "conv3_dgrad": [("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 3, false, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 1, false, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 3, false>", 0),
                     ("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 1, false>", 0)],
     "conv2_wgrad": [("conv_wgrad_trp_kernel<6, 64, 5, 11, 3, false>", 0),
                     ("conv_wgrad_trp_kernel<6, 64, 5, 11, 1, true>", 0)],
-    "conv2_dgrad": [("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false>", 0),
+    "conv2_dgrad": [("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 1, true, false>", 0),
+                    ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false>", 0),
                     ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 1, true>", 0)],
     "conv1_bwd_wgrad": [("conv1_wgrad_kernel<true>", 0)],
 }
