@@ -2204,6 +2204,189 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
   }
 }
 
+// Weight-stationary conv2 FORWARD with the A operand staged through LDS by DMA (ABD_WS_DMA=1,
+// A/B knob).  Same product, tiles, epilogue and summation order as conv_ws_split_kernel<EPI_CONV,
+// 2, 64, 1, .., KO = true>; only how the A fragments reach the registers differs.  The direct path
+// loads each lane's 32 B of its own output row from global memory: the four lanes of a quad (the
+// unit the texture address stage processes together) touch four NHWC rows 256 B apart -- four L1
+// lines per quad, ~58 tag lookups per 1-KB load, TA stalled on the L1 in 35 % of the kernel's
+// cycles.  Here, per 16-channel group, a wave DMAs the tile's whole source span (the 32 output
+// rows' positions plus the taps' +1 / +Ws / +Ws+1 shifts: <= 64 positions x 64 B) into its own
+// LDS buffer with `buffer_load_dwordx4 ... lds`, four lanes per position -- one line per quad --
+// and the four taps read their fragments from it (2 ds_read_b128 per lane and tap; the 16-B chunk
+// is XOR-swizzled by (position >> 2) & 3 so the 16 lanes of a read phase hit distinct banks).
+// Forward taps only ((0,0),(0,1),(1,0),(1,1) with Hs = Ho + 1, Ws = Wo + 1: every tap inside the
+// source), checked by the launcher.  No block barrier in the loop: each wave waits for its own DMA.
+constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31 + 3 + 14 + Ws + 1)
+template <int NP>
+__global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
+  constexpr int NJ = 2, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
+  __shared__ __attribute__((aligned(16))) float stage[WPB][kDmaSpan * 16];
+  __shared__ float red[WPB][N][2];
+  __shared__ float bfold[N];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
+    const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    bf16x8 pl[NP];
+    planes_x8<NP>(lo, hi, pl);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
+  }
+  if (a.fold_t != nullptr) {
+    for (int q = tid; q < N * 8; q += WPB * 64) {
+      const int n = q / 8, part = q % 8;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < CS / 8; ++c) acc += a.fold_t[(int64_t)(part * (CS / 8) + c) * N + n];
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) bfold[n] = (float)(acc + (double)a.bias[n]);
+    }
+  }
+  __syncthreads();
+  const int64_t W = (int64_t)gridDim.x * WPB;
+  const int64_t g = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(wave);
+  const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
+  const int HoWo = a.Ho * a.Wo;
+  const int npos = a.Hs * a.Ws * (a.M / HoWo);  // source positions
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
+  const int kq = 8 * (lane >> 5);
+  float st[NJ][2];
+  float bias[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    st[j][0] = st[j][1] = 0.0f;
+    bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
+  }
+  float* sw = stage[wave];
+  __attribute__((address_space(3))) void* swl = (__attribute__((address_space(3))) void*)sw;
+  // DMA of channel group cg for the span starting at source position p0: instruction i, lane l ->
+  // position 16 i + l / 4, LDS slot l % 4 holds global chunk (l % 4) ^ ((pos >> 2) & 3)
+  auto dma = [&](int p0, int cg) {
+#pragma unroll
+    for (int i = 0; i < kDmaSpan / 16; ++i) {
+      const int pos = 16 * i + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
+      const uint32_t off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (__attribute__((address_space(3))) void*)(sw + i * 256), 16,
+                                               (int)off, 0, 0, 0);
+    }
+  };
+  (void)swl;
+  const int ntiles = (r_hi - r_lo + 31) / 32;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  auto src_of = [&](int m) {
+    const int b = m / HoWo, rem = m - b * HoWo;
+    const int h = rem / a.Wo, w = rem - h * a.Wo;
+    return (b * a.Hs + h) * a.Ws + w;
+  };
+  const int tofs[4] = {0, 1, a.Ws, a.Ws + 1};  // forward taps (0,0) (0,1) (1,0) (1,1)
+  // B fragments of step (cg, t), double-buffered one step ahead (the LDS latency off the MFMA path)
+  bf16x8 bvs[2][NJ][NP];
+  auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
+    const int kb = t * CS + cg * 16 + kq;  // KO order: step = cg * 4 + t
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
+  };
+  int p0 = ntiles > 0 ? __builtin_amdgcn_readfirstlane(src_of(r_lo)) : 0;
+  if (ntiles > 0) dma(p0, 0);  // the first tile's group 0; later tiles' group 0 is issued a group ahead
+  load_b(0, 0, bvs[0]);
+#pragma unroll 1
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int m0 = r_lo + 32 * tile;
+    const int mr = min(m0 + (lane & 31), r_hi - 1);
+    const int prow = src_of(mr) - p0;  // this lane's row inside the span
+    const bool more = tile + 1 < ntiles;
+    const int p0n = __builtin_amdgcn_readfirstlane(src_of(more ? m0 + 32 : m0));
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+#pragma unroll
+    for (int cg = 0; cg < G; ++cg) {
+      // this wave's DMA of group cg has landed; group 0 of a later tile was issued before the
+      // previous tile's 32 epilogue stores, which may stay in flight (vmcnt counts in issue order)
+      if (cg == 0 && tile > 0) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 raw[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int pos = prow + tofs[t];
+        const int sx = (pos >> 2) & 3;
+        const float* rowp = sw + pos * 16;
+        raw[t][0] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5)) ^ sx) * 4));
+        raw[t][1] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5) + 1) ^ sx) * 4));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t == 1) {
+          // every lane's reads of group cg are complete (tap 0's MFMAs are issued: the wait costs
+          // little) before the buffer is refilled: with group cg + 1, or after the last group with
+          // the next tile's group 0
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (cg + 1 < G) dma(p0, cg + 1);
+          else if (more) dma(p0n, 0);
+        }
+        const int s = cg * 4 + t;
+        // next step's B fragments (past the tile's last step: the next tile's first)
+        load_b(((s + 1) % (4 * G)) / 4, (s + 1) % 4, bvs[(s + 1) & 1]);
+        bf16x8 av[NP];
+        planes_x8<NP>(__builtin_bit_cast(float4, raw[t][0]), __builtin_bit_cast(float4, raw[t][1]), av);
+        bf16x8 (&bv)[NJ][NP] = bvs[s & 1];
+#pragma unroll
+        for (int term = 0; term < Terms<NP>::n; ++term)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
+      }
+    }
+    p0 = p0n;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const bool ok = m < r_hi;
+      const uint32_t ob = ok ? (uint32_t)((m - r_lo) * N + (lane & 31)) * 4u : kOOB;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float v = fmaxf(acc[j][r] + bias[j], 0.0f);
+        const float vs = ok ? v : 0.0f;
+        st[j][0] += vs;
+        st[j][1] = fmaf(vs, vs, st[j][1]);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
+      }
+    }
+  }
+  if (a.part == nullptr) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+    const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+    if (lane < 32) {
+      red[wave][32 * j + lane][0] = s0;
+      red[wave][32 * j + lane][1] = s1;
+    }
+  }
+  __syncthreads();
+  if (tid < N) {
+    float s0 = 0.0f, s1 = 0.0f;
+    for (int w = 0; w < WPB; ++w) {
+      s0 += red[w][tid][0];
+      s1 += red[w][tid][1];
+    }
+    a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
+    a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
+  }
+}
+
 // Halo-tiled 2x2 conv GEMM, 3-plane split (ABD_PREC_F32_SPLIT), Cs = N = 64: conv2 forward and
 // data gradient.  The 128 output rows of a block (consecutive m, possibly across two images) read
 // source positions inside one contiguous span of whole source rows [s_lo, s_hi); per 32-channel
@@ -3970,7 +4153,16 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // tap-major everywhere / forward only / both
   static const int kord = env_int("ABD_WS_KORD", 1);
   const bool ko = kord == 2 || (kord == 1 && EPI == EPI_CONV);
-  if (PA) {
+  // LDS-DMA A operand for the forward (conv_ws_dma_kernel): conv2 fwd 0.141 -> 0.130 ms (A/B, one
+  // box); ABD_WS_DMA=0 restores the direct-load kernel
+  static const bool dma = env_int("ABD_WS_DMA", 1) != 0;
+  const bool fwd_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == 1 && a.dh[2] == 1 && a.dw[2] == 0 &&
+                        a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
+  // staged span of a 32-row tile: 31 steps, +1 per output-row end, +Ws(Hs-Ho) per image end, taps
+  const int span = 31 + (32 / a.Wo + 1) * (a.Ws - a.Wo) + (32 / (a.Ho * a.Wo) + 1) * ((a.Hs - a.Ho) * a.Ws) + a.Ws + 2;
+  if (EPI == EPI_CONV && !PA && dma && fwd_taps && a.N == 64 && a.Cs == 64 && span <= kDmaSpan) {
+    conv_ws_dma_kernel<NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  } else if (PA) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
