@@ -22,6 +22,9 @@
 #include <type_traits>
 #include <cmath>
 #include <vector>
+#include <map>
+#include <array>
+#include <mutex>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -2218,7 +2221,7 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
 // Forward taps only ((0,0),(0,1),(1,0),(1,1) with Hs = Ho + 1, Ws = Wo + 1: every tap inside the
 // source), checked by the launcher.  No block barrier in the loop: each wave waits for its own DMA.
 constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31 + 3 + 14 + Ws + 1)
-template <int NP>
+template <int EPI, int NP>
 __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   constexpr int NJ = 2, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
@@ -2235,7 +2238,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
   }
-  if (a.fold_t != nullptr) {
+  if (EPI == EPI_CONV && a.fold_t != nullptr) {
     for (int q = tid; q < N * 8; q += WPB * 64) {
       const int n = q / 8, part = q % 8;
       double acc = 0.0;
@@ -2252,6 +2255,13 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
   const int HoWo = a.Ho * a.Wo;
   const int npos = a.Hs * a.Ws * (a.M / HoWo);  // source positions
+  // taps as linear source offsets; the data gradient's leave the source grid at its edges (masked)
+  int tofs[4], tmin = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    tofs[t] = a.dh[t] * a.Ws + a.dw[t];
+    tmin = min(tmin, tofs[t]);
+  }
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
   const int kq = 8 * (lane >> 5);
@@ -2260,7 +2270,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     st[j][0] = st[j][1] = 0.0f;
-    bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
+    bias[j] = 0.0f;
+    if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
   }
   float* sw = stage[wave];
   __attribute__((address_space(3))) void* swl = (__attribute__((address_space(3))) void*)sw;
@@ -2286,7 +2297,26 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
     const int h = rem / a.Wo, w = rem - h * a.Wo;
     return (b * a.Hs + h) * a.Ws + w;
   };
-  const int tofs[4] = {0, 1, a.Ws, a.Ws + 1};  // forward taps (0,0) (0,1) (1,0) (1,1)
+  // tap-validity bits of output row m (h + dh in [0, Hs), w + dw in [0, Ws))
+  auto taps_of = [&](int m) {
+    const int b = m / HoWo, rem = m - b * HoWo;
+    const int h = rem / a.Wo, w = rem - h * a.Wo;
+    uint32_t mk = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int hs = h + a.dh[t], ws = w + a.dw[t];
+      if (hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
+    }
+    return mk;
+  };
+  // first staged position of the tile starting at m: the rows' minimum source index (a source
+  // image boundary can step it back) plus the most negative tap
+  auto span_base = [&](int m) {
+    int v = src_of(min(m + (lane & 31), r_hi - 1));
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v) + tmin;
+  };
   // B fragments of step (cg, t), double-buffered one step ahead (the LDS latency off the MFMA path)
   bf16x8 bvs[2][NJ][NP];
   auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
@@ -2296,7 +2326,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
       for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
   };
-  int p0 = ntiles > 0 ? __builtin_amdgcn_readfirstlane(src_of(r_lo)) : 0;
+  int p0 = ntiles > 0 ? span_base(r_lo) : 0;
   if (ntiles > 0) dma(p0, 0);  // the first tile's group 0; later tiles' group 0 is issued a group ahead
   load_b(0, 0, bvs[0]);
 #pragma unroll 1
@@ -2304,8 +2334,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
     const int m0 = r_lo + 32 * tile;
     const int mr = min(m0 + (lane & 31), r_hi - 1);
     const int prow = src_of(mr) - p0;  // this lane's row inside the span
+    const uint32_t tm = taps_of(mr);
     const bool more = tile + 1 < ntiles;
-    const int p0n = __builtin_amdgcn_readfirstlane(src_of(more ? m0 + 32 : m0));
+    const int p0n = span_base(more ? m0 + 32 : m0);
     f32x16 acc[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -2320,11 +2351,14 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
       uint4 raw[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int pos = prow + tofs[t];
+        const int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);  // an invalid tap's position is clamped
         const int sx = (pos >> 2) & 3;
         const float* rowp = sw + pos * 16;
         raw[t][0] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5)) ^ sx) * 4));
         raw[t][1] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5) + 1) ^ sx) * 4));
+        if constexpr (EPI != EPI_CONV) {  // and zeroed (forward taps never leave the grid)
+          if (!((tm >> t) & 1u)) raw[t][0] = raw[t][1] = make_uint4(0u, 0u, 0u, 0u);
+        }
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -2357,15 +2391,18 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
       const uint32_t ob = ok ? (uint32_t)((m - r_lo) * N + (lane & 31)) * 4u : kOOB;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        float v = fmaxf(acc[j][r] + bias[j], 0.0f);
-        const float vs = ok ? v : 0.0f;
-        st[j][0] += vs;
-        st[j][1] = fmaf(vs, vs, st[j][1]);
+        float v = acc[j][r];
+        if constexpr (EPI == EPI_CONV) {
+          v = fmaxf(v + bias[j], 0.0f);
+          const float vs = ok ? v : 0.0f;
+          st[j][0] += vs;
+          st[j][1] = fmaf(vs, vs, st[j][1]);
+        }
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
       }
     }
   }
-  if (a.part == nullptr) return;
+  if (EPI != EPI_CONV || a.part == nullptr) return;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
@@ -4139,6 +4176,38 @@ int ws_blocks(int N, int Cs, int64_t M) {
   const int64_t need = (M + 8 * 32 * (int64_t)mt - 1) / (8 * 32 * (int64_t)mt);  // 8-wave blocks
   return (int)std::max<int64_t>(1, std::min<int64_t>(full, need));
 }
+// Largest staged span (positions) of any 32 consecutive output rows of conv_ws_dma_kernel: the
+// rows' source indices repeat with the image (period Ho*Wo), so every window over two images plus
+// one tile is scanned once per geometry (cached).
+int dma_span(const NTArgs& a) {
+  static std::mutex mu;
+  static std::map<std::array<int, 12>, int> cache;
+  const std::array<int, 12> key{a.Hs, a.Ws, a.Ho, a.Wo, a.dh[0], a.dh[1], a.dh[2], a.dh[3], a.dw[0], a.dw[1], a.dw[2], a.dw[3]};
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const int HoWo = a.Ho * a.Wo, n = 2 * HoWo + 32;
+  int tmin = 0, tmax = 0;
+  for (int t = 0; t < 4; ++t) {
+    tmin = std::min(tmin, a.dh[t] * a.Ws + a.dw[t]);
+    tmax = std::max(tmax, a.dh[t] * a.Ws + a.dw[t]);
+  }
+  auto src = [&](int m) {
+    const int b = m / HoWo, rem = m % HoWo, h = rem / a.Wo, w = rem % a.Wo;
+    return (b * a.Hs + h) * a.Ws + w;
+  };
+  int span = 0;
+  for (int m0 = 0; m0 + 32 <= n; ++m0) {
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int r = 0; r < 32; ++r) {
+      lo = std::min(lo, src(m0 + r));
+      hi = std::max(hi, src(m0 + r));
+    }
+    span = std::max(span, hi + tmax - (lo + tmin) + 1);
+  }
+  cache[key] = span;
+  return span;
+}
 template <int EPI, int NP = 3, bool PA = false>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
@@ -4153,15 +4222,19 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // tap-major everywhere / forward only / both
   static const int kord = env_int("ABD_WS_KORD", 1);
   const bool ko = kord == 2 || (kord == 1 && EPI == EPI_CONV);
-  // LDS-DMA A operand for the forward (conv_ws_dma_kernel): conv2 fwd 0.141 -> 0.130 ms (A/B, one
-  // box); ABD_WS_DMA=0 restores the direct-load kernel
-  static const bool dma = env_int("ABD_WS_DMA", 1) != 0;
+  // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the data gradient
+  // measured slower through it (0.132 -> 0.141 ms: its tap masks and edge rows), so it stays on the
+  // direct kernel.  ABD_WS_DMA = 0 / 1 / 2: direct everywhere / DMA forward (default) / DMA both
+  static const int dma_mode = env_int("ABD_WS_DMA", 1);
+  const bool dma = dma_mode == 2 || (dma_mode == 1 && EPI == EPI_CONV);
+  // the forward's taps never leave the source grid; the data gradient's are masked in the kernel
   const bool fwd_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == 1 && a.dh[2] == 1 && a.dw[2] == 0 &&
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
-  // staged span of a 32-row tile: 31 steps, +1 per output-row end, +Ws(Hs-Ho) per image end, taps
-  const int span = 31 + (32 / a.Wo + 1) * (a.Ws - a.Wo) + (32 / (a.Ho * a.Wo) + 1) * ((a.Hs - a.Ho) * a.Ws) + a.Ws + 2;
-  if (EPI == EPI_CONV && !PA && dma && fwd_taps && a.N == 64 && a.Cs == 64 && span <= kDmaSpan) {
-    conv_ws_dma_kernel<NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  const bool dg_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == -1 && a.dh[2] == -1 && a.dw[2] == 0 &&
+                       a.dh[3] == -1 && a.dw[3] == -1;
+  if (!PA && dma && a.N == 64 && a.Cs == 64 && (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) &&
+      dma_span(a) <= kDmaSpan) {
+    conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
