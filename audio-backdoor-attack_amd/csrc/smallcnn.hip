@@ -179,6 +179,9 @@ struct BCoef {
 #ifndef ABD_C1_DD
 #define ABD_C1_DD 0
 #endif
+#ifndef ABD_C1W_U
+#define ABD_C1W_U 4  // pool windows per thread whose gradient loads conv1_wgrad_kernel batches
+#endif
 __device__ __forceinline__ float bn_dx(float dy, float r, float4 /*cf*/, const BCoef& bc) {
   return (float)fma(bc.B, (double)r, fma(bc.g, (double)dy, bc.A));
 }
@@ -660,12 +663,32 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
     const int b = chunk / nbh, h0 = (chunk % nbh) * a.rows;
     stage_x(a, b, h0, xs);
     const int rows = min(a.rows, a.g.H1 - h0);
+    const int nwin = rows * NW;
+    constexpr int WS = kT / 32;  // windows in flight per block
     int hl = pl / NW, wo = pl - hl * NW;  // (hl, wo) of idx, stepped without dividing by NW
-    for (int idx = pl; idx < rows * NW; idx += kT / 32, wo += kT / 32) {
-      while (wo >= NW) {
-        wo -= NW;
-        ++hl;
+    // ABD_C1W_U windows per thread per batch: their pooled-gradient loads are all issued before
+    // the first window's arithmetic (one exposed load latency per batch instead of per window);
+    // windows are still accumulated in idx order, so the sums are those of the one-window loop
+    for (int base = pl; base < nwin; base += ABD_C1W_U * WS) {
+      int hls[ABD_C1W_U], wos[ABD_C1W_U];
+      float2 dvs[ABD_C1W_U];
+  #pragma unroll
+      for (int u = 0; u < ABD_C1W_U; ++u) {
+        hls[u] = hl;
+        wos[u] = wo;
+        const bool ld = base + u * WS < nwin && (FULL || wo < a.g.W1p);
+        dvs[u] = ld ? *reinterpret_cast<const float2*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c0)
+                    : float2{0.0f, 0.0f};
+        wo += WS;
+        while (wo >= NW) {
+          wo -= NW;
+          ++hl;
+        }
       }
+  #pragma unroll
+      for (int u = 0; u < ABD_C1W_U; ++u) {
+      if (base + u * WS >= nwin) break;
+      const int hl = hls[u], wo = wos[u];
       const int w = 3 * wo;
       const int nw = FULL ? 3 : min(3, a.g.W1 - w);
       const bool real = FULL || wo < a.g.W1p;
@@ -676,14 +699,7 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
         xv[0][j] = (j <= nw) ? x0[j] : 0.0f;
         xv[1][j] = (j <= nw) ? x0[a.g.W0 + j] : 0.0f;
       }
-      float dd[CPT];
-      if (real) {
-        const float2 d2 = *reinterpret_cast<const float2*>(a.dp1 + (((int64_t)b * a.g.H1 + h0 + hl) * a.g.W1p + wo) * 64 + c0);
-        dd[0] = d2.x;
-        dd[1] = d2.y;
-      } else {
-        dd[0] = dd[1] = 0.0f;
-      }
+      const float dd[CPT] = {dvs[u].x, dvs[u].y};
       // the channel pair on v_pk_fma_f32: per channel the same fma chain as the oracle replay
       // (b, w00, w01, w10, w11) and the same accumulation order
       float r[CPT][3];
@@ -725,6 +741,7 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
         vp[2] = __builtin_elementwise_fma(dz, c1f2{xv[1][j], xv[1][j]}, vp[2]);
         vp[3] = __builtin_elementwise_fma(dz, c1f2{xv[1][j + 1], xv[1][j + 1]}, vp[3]);
         vp[4] += dz;
+      }
       }
     }
     __syncthreads();  // xs is restaged by the next chunk
@@ -2220,6 +2237,9 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
 // is XOR-swizzled by (position >> 2) & 3 so the 16 lanes of a read phase hit distinct banks).
 // Forward taps only ((0,0),(0,1),(1,0),(1,1) with Hs = Ho + 1, Ws = Wo + 1: every tap inside the
 // source), checked by the launcher.  No block barrier in the loop: each wave waits for its own DMA.
+#ifndef ABD_DMA_TRIM
+#define ABD_DMA_TRIM 1
+#endif
 constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31 + 3 + 14 + Ws + 1)
 template <int EPI, int NP>
 __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
@@ -2256,11 +2276,12 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   const int HoWo = a.Ho * a.Wo;
   const int npos = a.Hs * a.Ws * (a.M / HoWo);  // source positions
   // taps as linear source offsets; the data gradient's leave the source grid at its edges (masked)
-  int tofs[4], tmin = 0;
+  int tofs[4], tmin = 0, tmax = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     tofs[t] = a.dh[t] * a.Ws + a.dw[t];
     tmin = min(tmin, tofs[t]);
+    tmax = max(tmax, tofs[t]);
   }
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
@@ -2277,9 +2298,11 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   __attribute__((address_space(3))) void* swl = (__attribute__((address_space(3))) void*)sw;
   // DMA of channel group cg for the span starting at source position p0: instruction i, lane l ->
   // position 16 i + l / 4, LDS slot l % 4 holds global chunk (l % 4) ^ ((pos >> 2) & 3)
-  auto dma = [&](int p0, int cg) {
+  // only the 16-position blocks the tile reads (need: wave-uniform; typically 48 of the 64 slots)
+  auto dma = [&](int p0, int cg, int need) {
 #pragma unroll
     for (int i = 0; i < kDmaSpan / 16; ++i) {
+      if (i > 0 && 16 * i >= need) break;
       const int pos = 16 * i + (lane >> 2);
       const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
       const uint32_t off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
@@ -2311,11 +2334,18 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   };
   // first staged position of the tile starting at m: the rows' minimum source index (a source
   // image boundary can step it back) plus the most negative tap
-  auto span_base = [&](int m) {
-    int v = src_of(min(m + (lane & 31), r_hi - 1));
+  // and the number of staged positions its rows' taps reach (ABD_DMA_TRIM=0: always kDmaSpan)
+  auto span_base = [&](int m, int& need) {
+    const int s0 = src_of(min(m + (lane & 31), r_hi - 1));
+    int v = s0, u = s0;
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return __builtin_amdgcn_readfirstlane(v) + tmin;
+    for (int o = 16; o > 0; o >>= 1) {
+      v = min(v, __shfl_xor(v, o, 64));
+      u = max(u, __shfl_xor(u, o, 64));
+    }
+    const int base = __builtin_amdgcn_readfirstlane(v) + tmin;
+    need = ABD_DMA_TRIM ? __builtin_amdgcn_readfirstlane(u) + tmax + 1 - base : kDmaSpan;
+    return base;
   };
   // B fragments of step (cg, t), double-buffered one step ahead (the LDS latency off the MFMA path)
   bf16x8 bvs[2][NJ][NP];
@@ -2326,8 +2356,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
       for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
   };
-  int p0 = ntiles > 0 ? span_base(r_lo) : 0;
-  if (ntiles > 0) dma(p0, 0);  // the first tile's group 0; later tiles' group 0 is issued a group ahead
+  int need = kDmaSpan, needn = kDmaSpan;
+  int p0 = ntiles > 0 ? span_base(r_lo, need) : 0;
+  if (ntiles > 0) dma(p0, 0, need);  // the first tile's group 0; later tiles' group 0 is issued a group ahead
   load_b(0, 0, bvs[0]);
 #pragma unroll 1
   for (int tile = 0; tile < ntiles; ++tile) {
@@ -2336,7 +2367,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
     const int prow = src_of(mr) - p0;  // this lane's row inside the span
     const uint32_t tm = taps_of(mr);
     const bool more = tile + 1 < ntiles;
-    const int p0n = span_base(more ? m0 + 32 : m0);
+    const int p0n = span_base(more ? m0 + 32 : m0, needn);
     f32x16 acc[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -2367,8 +2398,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
           // little) before the buffer is refilled: with group cg + 1, or after the last group with
           // the next tile's group 0
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (cg + 1 < G) dma(p0, cg + 1);
-          else if (more) dma(p0n, 0);
+          if (cg + 1 < G) dma(p0, cg + 1, need);
+          else if (more) dma(p0n, 0, needn);
         }
         const int s = cg * 4 + t;
         // next step's B fragments (past the tile's last step: the next tile's first)
@@ -2384,6 +2415,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
       }
     }
     p0 = p0n;
+    need = needn;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);

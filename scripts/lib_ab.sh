@@ -21,6 +21,6 @@ for rep in 1 2; do
     echo "== bench $v rep $rep $(date +%T)"
     ABD_LIB=$(lib $v) timeout -k 10 240 python bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu ${BENCH_ARGS:-} \
       > "$O/${v}_$rep.json" 2> "$O/${v}_$rep.err" || { tail -20 "$O/${v}_$rep.err"; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); ph=d['phases_ms_per_launch']; print('  ms/step', d['ms_per_step'], 'stft', round(ph['stft_mel']*1000,1))" "$O/${v}_$rep.json"
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); ph=d['phases_ms_per_launch']; print('  ms/step', d['ms_per_step'], {k: round(v*1000,1) for k,v in ph.items()})" "$O/${v}_$rep.json"
   done
 done

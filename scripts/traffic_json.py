@@ -32,7 +32,8 @@ PHASE_KERNELS = {
                  ("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
     "db_dct": [("db_dct_mfma_kernel<3>", 0)],
     "conv1_stats": [("conv1_stats_fold_kernel", 0), ("conv1_stats_kernel", 0)],
-    "conv2_fwd": [("conv_ws_dma_kernel<3>", 0), ("conv_ws_dma_kernel<1>", 0),
+    "conv2_fwd": [("conv_ws_dma_kernel<1, 3>", 0), ("conv_ws_dma_kernel<1, 1>", 0),
+                  ("conv_ws_dma_kernel<3>", 0), ("conv_ws_dma_kernel<1>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false, true>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, true, true>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 3, false>", 0),
