@@ -2241,9 +2241,9 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
 #define ABD_DMA_TRIM 1
 #endif
 constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31 + 3 + 14 + Ws + 1)
-template <int EPI, int NP>
+template <int EPI, int NP, int NJ = 2>
 __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
-  constexpr int NJ = 2, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
+  constexpr int CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
   __shared__ __attribute__((aligned(16))) float stage[WPB][kDmaSpan * 16];
   __shared__ float red[WPB][N][2];
@@ -4264,9 +4264,12 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
   const bool dg_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == -1 && a.dh[2] == -1 && a.dw[2] == 0 &&
                        a.dh[3] == -1 && a.dw[3] == -1;
-  if (!PA && dma && a.N == 64 && a.Cs == 64 && (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) &&
-      dma_span(a) <= kDmaSpan) {
-    conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+  // conv3 (N = 32) through the same kernel with one 32-column tile per wave (ABD_WS_DMA3=0: direct)
+  static const bool dma3 = env_int("ABD_WS_DMA3", 1) != 0;
+  if (!PA && dma && (a.N == 64 || (a.N == 32 && dma3)) && a.Cs == 64 &&
+      (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
+    if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else conv_ws_dma_kernel<EPI, NP, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
