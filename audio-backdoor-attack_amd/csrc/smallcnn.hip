@@ -3542,18 +3542,41 @@ __global__ void __launch_bounds__(kT) fc2_reduce_colsum_kernel(const float* part
 }
 
 // ------------------------------------------------------------------ Adam (torch single-tensor semantics)
-__global__ void __launch_bounds__(kT) adam_kernel(float* p, const float* g, float* m, float* v, int64_t n,
-                                                  float omb1, float beta2, float omb2, float step_size,
-                                                  float bc2_sqrt, float eps) {
-  for (int64_t i = blockIdx.x * (int64_t)kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-    const float gi = g[i];
-    const float mi = m[i] + omb1 * (gi - m[i]);
-    const float vi = v[i] * beta2 + omb2 * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = p[i] + (-step_size) * (mi / denom);
+struct AdamArgs {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+  float omb1, beta2, omb2, step_size, bc2_sqrt, eps;
+};
+__device__ __forceinline__ void adam_elem(const AdamArgs& a, int64_t i) {
+  const float gi = a.g[i];
+  const float mi = a.m[i] + a.omb1 * (gi - a.m[i]);
+  const float vi = a.v[i] * a.beta2 + a.omb2 * gi * gi;
+  a.m[i] = mi;
+  a.v[i] = vi;
+  const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+  a.p[i] = a.p[i] + (-a.step_size) * (mi / denom);
+}
+__global__ void __launch_bounds__(kT) adam_kernel(AdamArgs a) {
+  for (int64_t i = blockIdx.x * (int64_t)kT + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kT) adam_elem(a, i);
+}
+// The single-rank train step's last two launches in one: blocks [0, 320) reduce one conv1 weight /
+// bias gradient column each from conv1_wgrad_kernel's partials (partial_sum_body: the gradient
+// buffer gets the same value) and apply Adam to that parameter; the other blocks run Adam over
+// parameters [320, n).  conv1.weight / conv1.bias are the flat buffer's first 256 + 64 entries.
+__global__ void __launch_bounds__(kT) adam_c1_kernel(AdamArgs a, const float* part, int nblk) {
+  constexpr int kC1 = 5 * 64;
+  if ((int)blockIdx.x < kC1) {
+    const int col = blockIdx.x;
+    float* g = const_cast<float*>(a.g);
+    partial_sum_body(part, nblk, nullptr, g, g + 4 * 64, col);
+    if (threadIdx.x == 0) adam_elem(a, col < 4 * 64 ? (col % 64) * 4 + col / 64 : col);
+    return;
   }
+  const int64_t nb = (int64_t)gridDim.x - kC1;
+  for (int64_t i = kC1 + ((int64_t)blockIdx.x - kC1) * kT + threadIdx.x; i < a.n; i += nb * kT) adam_elem(a, i);
 }
 
 // d z = d o - exp(o) * sum(d o)   (o = log_softmax(z))
@@ -4758,7 +4781,9 @@ int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, d
 int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const float* x, int64_t B,
              const DropArgs& drop1, hipStream_t s, void* fc_grads_event, const BnSync& sy = BnSync{},
              int64_t* metrics = nullptr, bool fold1 = false, double loss_w = 1.0, const HeadArgs* head = nullptr,
-             int planes = 0) {
+             int planes = 0, int* c1_defer = nullptr) {
+  // c1_defer != nullptr: conv1's weight / bias gradient columns are left as partials in w.part (their
+  // count in *c1_defer) for adam_c1_kernel to reduce in the optimizer launch
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   // head: the fused fc head ran its forward and row launches (fc_head.inc); its third launch -- fc
   // gradients, counters, BN3 backward -- replaces everything down to conv3's weight gradient
@@ -5064,8 +5089,12 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_CONV1_BWD, s);
     ABD_LAUNCH_CHECK();
     // part rows: j*64 + c, j = 0..3 weights (kh,kw), 4 bias -> conv1.w is (c,1,kh,kw): transpose via tiny pass
-    partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, nullptr, G[P_C1W], G[P_C1B]);
-    ABD_LAUNCH_CHECK();
+    if (c1_defer != nullptr) {
+      *c1_defer = c1.nblk;
+    } else {
+      partial_sum_kernel<<<5 * 64, kT, 0, s>>>(w.part, c1.nblk, 5 * 64, nullptr, G[P_C1W], G[P_C1B]);
+      ABD_LAUNCH_CHECK();
+    }
   }
   return stream_dep(net->ev_join, sw, s);
 }
@@ -5198,11 +5227,26 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
     // the metrics reduction rides on backward()'s fc2 gradient launch
     if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
   }
+  // single-rank update: conv1's gradient reduction rides on the Adam launch (one launch fewer)
+  static const bool fuse_c1 = env_int("ABD_ADAM_C1", 1) != 0;
+  const bool defer = fuse_c1 && a->do_update && !sy.on() && net->off[P_C1W] == 0 && net->off[P_C1B] == 4 * 64 &&
+                     net->off[P_BN1W] == 5 * 64;
+  int c1_nblk = 0;
   if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w,
-               use_head ? &ha : nullptr, planes))
+               use_head ? &ha : nullptr, planes, defer ? &c1_nblk : nullptr))
     return -1;
   copy_masks(a, w, g, B, s);
-  if (a->do_update) {
+  if (defer) {
+    const double bc1 = 1.0 - pow((double)a->beta1, (double)a->adam_step);
+    const double bc2 = 1.0 - pow((double)a->beta2, (double)a->adam_step);
+    const int64_t n = net->off[P_COUNT];
+    const AdamArgs aa{a->params, a->grads, a->exp_avg, a->exp_avg_sq, n, (float)(1.0 - (double)a->beta1), a->beta2,
+                      (float)(1.0 - (double)a->beta2), (float)((double)a->lr / bc1), (float)sqrt(bc2), a->eps};
+    abd::prof_begin(abd::PH_ADAM, s);
+    adam_c1_kernel<<<5 * 64 + (unsigned)grid_for(n - 5 * 64, 2048), kT, 0, s>>>(aa, w.part, c1_nblk);
+    abd::prof_end(abd::PH_ADAM, s);
+    ABD_LAUNCH_CHECK();
+  } else if (a->do_update) {
     int rc = abd_smallcnn_apply(net, a, workspace, workspace_bytes, stream);
     if (rc) return rc;
   }
@@ -5415,9 +5459,10 @@ int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_a
   const float step_size = (float)((double)lr / bc1);
   const float bc2s = (float)sqrt(bc2);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const AdamArgs aa{params, grads, exp_avg, exp_avg_sq, n, (float)(1.0 - (double)beta1), beta2,
+                    (float)(1.0 - (double)beta2), step_size, bc2s, eps};
   abd::prof_begin(abd::PH_ADAM, s);
-  adam_kernel<<<grid_for(n, 2048), kT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, n, (float)(1.0 - (double)beta1),
-                                               beta2, (float)(1.0 - (double)beta2), step_size, bc2s, eps);
+  adam_kernel<<<grid_for(n, 2048), kT, 0, s>>>(aa);
   abd::prof_end(abd::PH_ADAM, s);
   ABD_LAUNCH_CHECK();
   return ABD_OK;
