@@ -534,7 +534,12 @@ __device__ __forceinline__ bool guard_last_block(unsigned* ticket) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (t == gridDim.x - 1) ? 1u : 0u;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // every block has taken its ticket: re-arm it, so a launch that finds no prep block before it
+      // (a second abd_smallcnn_backward after one forward) still sees a zeroed ticket
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2376,9 +2381,16 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
     for (int cg = 0; cg < G; ++cg) {
       // this wave's DMA of group cg has landed; group 0 of a later tile was issued before the
-      // previous tile's 32 epilogue stores, which may stay in flight (vmcnt counts in issue order)
-      if (cg == 0 && tile > 0) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // previous tile's 16 * NJ epilogue stores, which may stay in flight (vmcnt counts in issue
+      // order).  The count must equal the stores per tile exactly: a larger one lets the DMA
+      // of group 0 still be in flight (NJ = 1 issues 16 stores: vmcnt(32) would never wait).
+      static_assert(NJ == 1 || NJ == 2, "epilogue store count per tile is 16 * NJ");
+      if (cg == 0 && tile > 0) {
+        if constexpr (NJ == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       uint4 raw[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -3601,7 +3613,7 @@ struct abd_cnn {
   Geo g;
   int max_batch;
   int64_t off[P_COUNT + 1];
-  int precision = ABD_PREC_F32;  // ABD_PREC_BF16: conv2/conv3 fwd + dgrad on bf16 MFMA
+  int precision = ABD_PREC_F32_SPLIT;  // abd_smallcnn_set_precision (include/abd.h)
   // weight-gradient side stream (created on first use): conv3 / conv2 weight gradients run there,
   // concurrently with the data-gradient chain of the caller's stream, joined before return
   hipStream_t side = nullptr;
@@ -5257,7 +5269,7 @@ int abd_smallcnn_forward(abd_cnn* net, const abd_train_args* a, int train_mode, 
                          size_t workspace_bytes, abd_stream_t stream) {
   ABD_CHECK(net && a && a->x && a->params && a->running && a->logprobs_out, ABD_E_INVALID, "NULL argument");
   const int64_t B = a->batch;
-  ABD_CHECK(B >= (train_mode ? 2 : 1), ABD_E_INVALID, "bad batch %lld", (long long)B);
+  ABD_CHECK(B >= 1, ABD_E_INVALID, "bad batch %lld", (long long)B);  // 1 row: BatchNorm2d counts N x H x W
   ABD_CHECK(B * net->g.H1 * net->g.W1p * 64 < (1LL << 31), ABD_E_INVALID, "batch too large (int32 activation offsets)");
   const Work w = layout(net, B, static_cast<char*>(workspace));
   ABD_CHECK(workspace && workspace_bytes >= w.bytes, ABD_E_WORKSPACE, "workspace too small (%zu < %zu)",

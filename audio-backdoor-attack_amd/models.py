@@ -3,7 +3,8 @@
 The module keeps the reference's submodule structure (conv1, bn1, pool1, ..., fc2,
 softmax) so construction consumes torch's RNG exactly like the reference (same
 initial weights under the same seed) and ``state_dict()`` keys/shapes are identical.
-Only ``forward`` differs: it runs libabd's fp32 MFMA kernels.
+Only ``forward`` differs: it runs libabd's HIP kernels (conv GEMMs in the fp32-accurate
+'f32split' mode by default, see ``set_gemm_precision``).
 
 On first use the parameters are re-homed into ONE flat device buffer (torch
 parameter order) and each ``nn.Parameter``'s ``.data`` becomes a view of it; BN
@@ -146,7 +147,7 @@ class smallcnn(nn.Module):
         self._engine = None
         self._step = 0
         self._dropout_nonce = None   # drawn at the first bind to the device (draw_dropout_nonce)
-        self.gemm_precision = "f32"   # "bf16": conv GEMMs on bf16 MFMA (set_gemm_precision)
+        self.gemm_precision = "f32split"  # conv GEMM mode (set_gemm_precision); "f32" / "bf16" opt-in
         self.dropout_source = "device"  # "torch_cpu": the reference CPU path's exact masks
 
     def set_dropout_source(self, source: str):
@@ -169,7 +170,7 @@ class smallcnn(nn.Module):
         # also the target of reference-format checkpoints (training.ReferencePickle), whose state is
         # a plain reference smallcnn's __dict__: fill in what this class adds
         super().__setstate__(state)
-        for k, v in (("_engine", None), ("_step", 0), ("gemm_precision", "f32"), ("dropout_source", "device"),
+        for k, v in (("_engine", None), ("_step", 0), ("gemm_precision", "f32split"), ("dropout_source", "device"),
                      ("_dropout_nonce", None)):
             if k not in self.__dict__:
                 self.__dict__[k] = v
@@ -184,10 +185,11 @@ class smallcnn(nn.Module):
 
     # ------------------------------------------------------------------ binding
     def set_gemm_precision(self, precision: str):
-        """'f32' (default, the reference's numerics: v_mfma_f32_32x32x2_f32), 'f32split' (the same
-        fp32-accurate products as exact three-way bf16 splits, six v_mfma_f32_32x32x16_bf16 terms)
-        or 'bf16' (operands rounded to bf16, fp32 accumulation; BASELINE configs[2]); applies to the
-        conv2/conv3 forward and data-gradient GEMMs."""
+        """'f32split' (default: fp32-accurate products as exact three-way bf16 splits, six
+        v_mfma_f32_32x32x16_bf16 terms, fp32 accumulation -- parity-tested at the fp32 tolerance and
+        the fastest fp32-accurate kernels), 'f32' (v_mfma_f32_32x32x2_f32, opt-in) or 'bf16'
+        (operands rounded to bf16, fp32 accumulation; BASELINE configs[2]/[4]); applies to the
+        conv2/conv3 forward, data- and weight-gradient GEMMs."""
         if precision not in L.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(L.PRECISIONS)}, got {precision!r}")
         self.gemm_precision = precision
@@ -238,7 +240,7 @@ class smallcnn(nn.Module):
                 new.nbt[i].copy_(bn.num_batches_tracked)
                 bn.num_batches_tracked = new.nbt[i]
                 o += 2 * c
-        new.apply_precision(getattr(self, "gemm_precision", "f32"))
+        new.apply_precision(getattr(self, "gemm_precision", "f32split"))
         self._engine = new
         return new
 

@@ -38,7 +38,7 @@ def n_frames(length, n_fft: int, hop: int):
     return 1 + (length + 2 * (n_fft // 2) - n_fft) // hop
 
 
-def _net(H0: int, W0: int, K: int, precision: str = "f32"):
+def _net(H0: int, W0: int, K: int, precision: str = "f32split"):
     """A cached libabd network handle for one geometry (no device state: shapes and precision)."""
     key = (int(H0), int(W0), int(K))
     h = _NETS.get(key)
@@ -111,13 +111,13 @@ def _eval(x, params, running, num_classes, precision, labels, indicators, metric
 
 
 @torch.library.custom_op("abd::smallcnn_eval", mutates_args=())
-def smallcnn_eval(x: Tensor, params: Tensor, running: Tensor, num_classes: int, precision: str = "f32") -> Tensor:
+def smallcnn_eval(x: Tensor, params: Tensor, running: Tensor, num_classes: int, precision: str = "f32split") -> Tensor:
     """model.eval() forward: (B, 1, H0, W0) -> log-probs (B, K); running BN statistics, no dropout."""
     return _eval(x, params, running, num_classes, precision, None, None, None)
 
 
 @smallcnn_eval.register_fake
-def _(x, params, running, num_classes, precision="f32"):
+def _(x, params, running, num_classes, precision="f32split"):
     return x.new_empty((x.shape[0], num_classes))
 
 
@@ -141,7 +141,7 @@ def smallcnn_train_step(x: Tensor, labels: Tensor, indicators: Optional[Tensor],
                         exp_avg: Tensor, exp_avg_sq: Tensor, running: Tensor, num_batches_tracked: Tensor,
                         metrics: Tensor, num_classes: int, adam_step: int, lr: float, beta1: float, beta2: float,
                         eps: float, seed: int, counter: int, mask1: Optional[Tensor] = None,
-                        mask2: Optional[Tensor] = None, precision: str = "f32", grad_scale: float = 1.0,
+                        mask2: Optional[Tensor] = None, precision: str = "f32split", grad_scale: float = 1.0,
                         row_offset: int = 0) -> Tensor:
     """One fused train() iteration on the device; returns the batch's log-probs (B, K).
 
@@ -171,7 +171,7 @@ def smallcnn_train_step(x: Tensor, labels: Tensor, indicators: Optional[Tensor],
 
 @smallcnn_train_step.register_fake
 def _(x, labels, indicators, params, grads, exp_avg, exp_avg_sq, running, num_batches_tracked, metrics, num_classes,
-      adam_step, lr, beta1, beta2, eps, seed, counter, mask1=None, mask2=None, precision="f32", grad_scale=1.0,
+      adam_step, lr, beta1, beta2, eps, seed, counter, mask1=None, mask2=None, precision="f32split", grad_scale=1.0,
       row_offset=0):
     return x.new_empty((x.shape[0], num_classes))
 

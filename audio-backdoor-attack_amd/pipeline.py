@@ -31,7 +31,7 @@ import torch
 
 from . import _lib as L
 from . import features as F
-from .models import smallcnn
+from .models import smallcnn, dropout_seed
 from . import training as T
 from . import parallel_dp as DP
 
@@ -160,10 +160,14 @@ class ResidentTrainer:
     def __init__(self, cfg: AttackConfig, waves: torch.Tensor, labels: torch.Tensor, model: smallcnn,
                  optimizer: torch.optim.Optimizer, batch_size: int, trigger: np.ndarray | None = None,
                  seed: int = 35, rank: int = 0, world: int = 1, process_group=None,
-                 gemm_precision: str | None = None, sync_bn: bool = False, poison_rows=None):
+                 gemm_precision: str | None = None, sync_bn: bool = False, poison_rows=None,
+                 collectives: bool | None = None):
         """batch_size is per rank (global batch = batch_size * world).  poison_rows: explicit
         poisoned rows (e.g. DABA's file-level schedule); default: the reference's own index work
-        (poison_schedule).  sync_bn: BatchNorm statistics over the global batch (world > 1)."""
+        (poison_schedule).  sync_bn: BatchNorm statistics over the global batch (world > 1).
+        collectives: run the data-parallel step (overlapped gradient all-reduce, SyncBN, separate
+        Adam) -- default world > 1; True at world 1 drives the same collectives over a one-rank
+        group (tests/test_gpu_rccl.py runs them through RCCL on a single GPU)."""
         assert waves.is_cuda and waves.dtype == torch.float32 and waves.dim() == 2
         self.cfg, self.model, self.opt = cfg, model, optimizer
         self.B, self.rank, self.world, self.pg = int(batch_size), rank, world, process_group
@@ -232,9 +236,15 @@ class ResidentTrainer:
         self._pos = 0
         self.reducer = None
         self.bn_sync = None
-        if world > 1:
-            # DDP semantics: every rank starts from rank 0's parameters and BN buffers
-            DP.broadcast_state([eng.params, eng.running, eng.nbt], 0, process_group)
+        self.dropout_seed = None  # None: models.dropout_seed per step (one rank)
+        self.dp = world > 1 if collectives is None else bool(collectives)
+        if self.dp:
+            # DDP semantics: every rank starts from rank 0's parameters and BN buffers -- and its
+            # dropout seed: the masks hash the GLOBAL batch row, so ranks seeded differently (a
+            # common seed + rank pattern) must still draw the 1-process run's masks
+            ds = torch.tensor([dropout_seed(self.dev, model)], dtype=torch.int64, device=self.dev)
+            DP.broadcast_state([eng.params, eng.running, eng.nbt, ds], 0, process_group)
+            self.dropout_seed = int(ds.item())
             split = int(eng.offsets[12])  # fc1.weight onwards (P_F1W)
             self.reducer = DP.OverlappedGradAllReduce(eng.grads, split, process_group)
             if sync_bn:
@@ -296,14 +306,14 @@ class ResidentTrainer:
     def _train(self, batch, x):
         _, lab, ind, _, _ = batch
         b = int(lab.numel())
-        if self.world == 1:
+        if not self.dp:
             T.train_step(self.model, x, lab, ind, self.adam, self.metrics)
             return
         g, row0 = self._cur
         if b > 0:
             T.train_step(self.model, x, lab, ind, self.adam, self.metrics, do_update=False,
                          grad_scale=DP.grad_scale(b, g), fc_grads_event=self.reducer.event_ptr(),
-                         row_offset=row0, bn_sync=self.bn_sync)
+                         row_offset=row0, bn_sync=self.bn_sync, seed=self.dropout_seed)
         else:
             # the tail batch has fewer rows than there are ranks: nothing to compute here, but this
             # rank joins every collective of the step with zero contributions
@@ -327,7 +337,7 @@ class ResidentTrainer:
 
     def read_metrics(self, reduce=True):
         m = self.metrics.clone()
-        if self.world > 1 and reduce:
+        if self.dp and reduce:
             m = DP.reduce_metrics(m, self.pg)
         loss_sum, total, correct, pt, ah, nb = T.read_metrics(m)
         return {"loss": loss_sum / max(nb, 1), "acc": 100.0 * correct / max(total, 1),
@@ -336,7 +346,7 @@ class ResidentTrainer:
     def sync_buffers(self):
         """DDP broadcast_buffers: BN running statistics from rank 0 (evaluation and checkpoints see
         one model on every rank; with sync_bn they are already identical)."""
-        if self.world > 1:
+        if self.dp:
             eng = self.model._engine
             DP.broadcast_state([eng.running, eng.nbt], 0, self.pg)
 

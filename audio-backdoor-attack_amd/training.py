@@ -11,9 +11,8 @@ element, training_tools.py:71-79).
 from __future__ import annotations
 
 import copy
-import copyreg
 import ctypes as C
-import importlib
+import pickle
 
 import numpy as np
 import torch
@@ -256,24 +255,43 @@ def clean_test(model, device, clean_test_loader, criterion):
 
 
 # ------------------------------------------------------------------ reference-format checkpoints
-class _ModuleRef:
-    """Unpickles as ``importlib.import_module(name)`` in the LOADING process."""
-
-    def __init__(self, name):
-        self.name = name
-
-    def __reduce__(self):
-        return (importlib.import_module, (self.name,))
+_GLOBAL_ATTR = "__abd_pickle_global__"
 
 
-class _ClassRef:
-    """Unpickles as ``getattr(import_module(module), name)``: the consumer's own class."""
+def _global_stub(module: str, name: str) -> type:
+    """A class that pickles as the opcode ``GLOBAL module name`` -- the reference class's own
+    import path -- without that module being importable (or imported) in the SAVING process."""
+    return type(name, (), {_GLOBAL_ATTR: (module, name), "__module__": module, "__qualname__": name})
 
-    def __init__(self, module, name):
-        self.module, self.name = module, name
 
-    def __reduce__(self):
-        return (getattr, (_ModuleRef(self.module), self.name))
+class _GlobalPickler(pickle._Pickler):
+    """The pure-Python pickler with one change: a ``_global_stub`` class is written as a plain
+    GLOBAL / STACK_GLOBAL of its target name (the stock pickler looks the name up and insists on
+    finding the very same object, which the stub is not).  Everything else -- torch's storages via
+    persistent_id, memo, opcodes -- is the standard protocol."""
+
+    def save_global(self, obj, name=None):
+        target = vars(obj).get(_GLOBAL_ATTR) if isinstance(obj, type) else None
+        if target is None:
+            return super().save_global(obj, name)
+        module, qual = target
+        if self.proto >= 4:
+            self.save(module)
+            self.save(qual)
+            self.write(pickle.STACK_GLOBAL)
+        else:
+            self.write(pickle.GLOBAL + f"{module}\n{qual}\n".encode("utf-8"))
+        self.memoize(obj)
+
+
+class _GlobalPickleModule:
+    """``pickle_module`` for torch.save: the standard module with the GLOBAL-writing Pickler."""
+    Pickler = _GlobalPickler
+    Unpickler = pickle.Unpickler
+    __name__ = "pickle"
+
+    def __getattr__(self, k):
+        return getattr(pickle, k)
 
 
 def reference_module_state(model: smallcnn) -> dict:
@@ -294,26 +312,28 @@ def reference_module_state(model: smallcnn) -> dict:
     return ref.__dict__.copy()
 
 
-class ReferencePickle:
-    """``torch.save(ReferencePickle(model), path)`` writes the whole-module pickle the reference's
-    ``torch.save(model)`` writes (utils/training_tools.py:49): loading it rebuilds the LOADER's
+def reference_pickle_object(model: smallcnn, module: str = "utils.models", name: str = "smallcnn"):
+    """An object that pickles exactly as the reference's ``torch.save(model)`` pickles its
+    ``utils.models.smallcnn`` (utils/training_tools.py:49): protocol 2's ``GLOBAL utils.models
+    smallcnn`` + ``NEWOBJ`` + ``BUILD`` of the module ``__dict__`` (reference_module_state).
+    Saved with ``pickle_module=_GlobalPickleModule``, loading it rebuilds the LOADER's
     ``utils.models.smallcnn`` -- the reference's class for its defenses (fp.py:125 then hooks and
     ``prune.custom_from_mask`` its submodules, fp.py:137,171; ft_reg.py:238, tsbd.py:256,
     correlation_analysis.py:128), this package's drop-in under ``abd_amd.run`` (flowmur.py:55) --
-    with nothing of abd_amd needed to unpickle it."""
-
-    def __init__(self, model: smallcnn, module: str = "utils.models", name: str = "smallcnn"):
-        self.model, self.module, self.name = model, module, name
-
-    def __reduce_ex__(self, protocol):
-        return (copyreg._reconstructor, (_ClassRef(self.module, self.name), object, None),
-                reference_module_state(self.model))
+    with nothing of abd_amd needed, and under ``torch.load(weights_only=True)`` once the consumer
+    allowlists the reference's classes (no import_module / getattr calls in the stream)."""
+    obj = object.__new__(_global_stub(module, name))
+    obj.__dict__.update(reference_module_state(model))
+    return obj
 
 
 def save_reference_checkpoint(model, path):
     """torch.save in the reference's format: abd smallcnn -> a utils.models.smallcnn pickle; any other
     module is saved as is (the reference's behaviour)."""
-    torch.save(ReferencePickle(model) if isinstance(model, smallcnn) else model, path)
+    if isinstance(model, smallcnn):
+        torch.save(reference_pickle_object(model), path, pickle_module=_GlobalPickleModule())
+    else:
+        torch.save(model, path)
 
 
 class EarlyStoppingModel:

@@ -151,10 +151,14 @@ def cpu_threads():
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
 
 
-def cpu_baseline(batch, threads, steps=2):
-    """The reference CPU path at the bench's batch: torch-fp32 restatement
-    (oracle/torch_ref.py: torch.stft MFCC with torchaudio's semantics + nn smallcnn with the
-    reference structure + torch Adam), ultrasonic K=35, 10 % poisoned; 1 warmup + `steps` timed."""
+def cpu_baseline(batch, threads, n_train=4096, n_test=1024, warmup_steps=2):
+    """The reference CPU path on the bench's workload, as a bounded sample: torch-fp32
+    restatement (oracle/torch_ref.py: torch.stft MFCC with torchaudio's semantics + nn smallcnn of the
+    reference structure + torch Adam), ultrasonic K = 35, 10 % of the training clips poisoned.  After
+    `warmup_steps` untimed steps, ONE full epoch over n_train clips at the bench batch is timed (per
+    batch, as in the GPU step: trigger add on the poisoned rows -> MFCC -> forward / CE / backward /
+    Adam -> counters); then test() on n_test clean clips and on the backdoor test set (the non-target
+    test clips with the trigger, labels 2) gives clean accuracy and ASR after that epoch."""
     import numpy as np
     import torch
     from oracle import torch_ref
@@ -164,33 +168,127 @@ def cpu_baseline(batch, threads, steps=2):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        n = 2 * batch
-        w, lab = synth.make_clips_np(n, 44100, 44100, 35, seed=123)
-        waves, labels = torch.from_numpy(w), torch.from_numpy(lab)
+        t_prep = time.perf_counter()
+        waves, labels = synth.make_clips_torch(n_train + n_test, 44100, 44100, 35, seed=123, device="cpu")
         trig = torch.from_numpy(ultrasonic_trigger_f32()[0])
         feat = torch_ref.MfccCPU(44100, 40, 1103, 441)
         torch.manual_seed(5)
         model = torch_ref.SmallCNN(35, 3072).train()
         opt = torch.optim.Adam(model.parameters(), lr=1e-4)
         g = torch.Generator().manual_seed(1)
+        tr_w, tr_y = waves[:n_train], labels[:n_train]
+        pois = torch.zeros(n_train, dtype=torch.bool)
+        pois[torch.randperm(n_train, generator=g)[: n_train // 10]] = True        # ultrasonic.py:70-71
+        y_eff = torch.where(pois, torch.full_like(tr_y, 2), tr_y)                  # :77
 
-        def step():
-            rows = torch.randint(0, n, (batch,), generator=g)
-            pois = torch.rand(batch, generator=g) < 0.1
-            x = waves[rows] + pois[:, None].float() * trig[None]      # ultrasonic.py:75 (poisoned rows)
-            y = torch.where(pois, torch.full_like(labels[rows], 2), labels[rows])
-            return torch_ref.train_step(model, opt, feat(x), y, pois.long())
-        step()
+        def step(rows):
+            x = tr_w[rows] + pois[rows, None].float() * trig[None]                 # ultrasonic.py:75
+            return torch_ref.train_step(model, opt, feat(x), y_eff[rows], pois[rows].long())
+        warm = torch.randperm(n_train, generator=g)
+        for k in range(warmup_steps):
+            step(warm[k * batch:(k + 1) * batch])
+        prep_s = time.perf_counter() - t_prep
+        perm = torch.randperm(n_train, generator=g)
+        loss, correct, ptot, phit, nb = 0.0, 0, 0, 0, 0
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
+        for s0 in range(0, n_train, batch):
+            l_, c_, p_, h_ = step(perm[s0:s0 + batch])
+            loss, correct, ptot, phit, nb = loss + l_, correct + c_, ptot + p_, phit + h_, nb + 1
         dt = time.perf_counter() - t0
+        model.eval()
+        te_w, te_y = waves[n_train:], labels[n_train:]
+        with torch.no_grad():
+            pred = torch.cat([model(feat(te_w[s:s + 256])).argmax(1) for s in range(0, n_test, 256)])
+            bd = te_y != 2                                                       # ultrasonic.py:90-102
+            bw = te_w[bd] + trig[None]
+            bpred = torch.cat([model(feat(bw[s:s + 256])).argmax(1) for s in range(0, bw.shape[0], 256)])
+        epoch = {"train_loss": round(loss / nb, 4), "train_acc": round(100.0 * correct / n_train, 3),
+                 "train_asr": round(100.0 * phit / max(ptot, 1), 3),
+                 "clean_acc": round(100.0 * float((pred == te_y).float().mean()), 3),
+                 "asr": round(100.0 * float((bpred == 2).float().mean()), 3)}
     finally:
         torch.set_num_threads(prev)
-    return {"value": round(batch * steps / dt, 2), "unit": "utterances/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} steps of batch {batch} after 1 warmup ({dt:.1f} s): ultrasonic clips (44.1 kHz x 1 s), "
-                      "trigger add + torch.stft MFCC(1103/441) + smallcnn fwd/bwd/Adam in torch fp32 on the host "
-                      "(oracle/torch_ref.py, the reference CPU path restated)"}
+    return {"value": round(n_train / dt, 2), "unit": "utterances/s", "cores": threads,
+            "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
+            "sample": f"one epoch of {n_train} clips at batch {batch} ({nb} steps, {dt:.1f} s) after {warmup_steps} "
+                      f"warmup steps: ultrasonic clips (44.1 kHz x 1 s, 10 % poisoned), trigger add + torch.stft "
+                      f"MFCC(1103/441) + smallcnn fwd/bwd/Adam in torch fp32 on {threads} host threads "
+                      f"(oracle/torch_ref.py, the reference CPU path restated); then test() on {n_test} clean clips "
+                      f"and {int(bd.sum())} backdoor clips",
+            "epoch_s": round(dt, 3), "setup_s": round(prep_s, 3), "after_epoch": epoch}
+
+
+def dropin_bench(cfg, waves, K, batch, nbatch, dev, precision):
+    """The unchanged attack scripts' loop (utils/training_tools.py:52-85 train(), badnets.py:146-160):
+    the drop-in ``train()`` over a DataLoader of precomputed (1, T, C) MFCC, per-batch H2D included --
+    against the same device step without the Python loop (what ResidentTrainer runs per batch after
+    its feature stage).  Four timings over `nbatch` batches of `batch` rows, each after a warmup:
+    cnn_step (training.train_step on device-resident batches: the resident CNN phases), dropin_device
+    (train() over already-resident batches: the drop-in's Python + custom-op dispatch around the same
+    step), dropin_loader (train() over the CPU DataLoader: + collation + H2D), loader_only."""
+    import torch
+    from abd_amd import features as F, training as T, _lib as L
+    from abd_amd.models import smallcnn
+
+    class DictSet(torch.utils.data.Dataset):   # prepare_dataset.py:13-33 item contract
+        def __init__(self, x, y, ind):
+            self.x, self.y, self.ind = x, y, ind
+
+        def __len__(self):
+            return len(self.x)
+
+        def __getitem__(self, i):
+            return {"mfcc": self.x[i], "label": self.y[i], "poison_indicator": self.ind[i]}
+
+    mcfg = cfg.mfcc()
+    n = batch * nbatch
+    rows = torch.arange(n, dtype=torch.int32, device=dev) % waves.shape[0]
+    xs = torch.cat([F.mfcc_batch(waves, mcfg, rows=rows[s:s + batch]) for s in range(0, n, batch)])
+    g = torch.Generator().manual_seed(3)
+    y = torch.randint(0, K, (n,), generator=g)
+    ind = (torch.rand(n, generator=g) < cfg.poisoning_rate).long()
+    y[ind == 1] = cfg.target_label
+    x_cpu = xs.cpu()
+    dev_batches = [{"mfcc": xs[s:s + batch], "label": y[s:s + batch].to(dev), "poison_indicator": ind[s:s + batch].to(dev)}
+                   for s in range(0, n, batch)]
+    loader = torch.utils.data.DataLoader(DictSet(x_cpu, y, ind), batch_size=batch, shuffle=True)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def fresh():
+        torch.manual_seed(35)
+        m = smallcnn(K, cfg.linear_features).to(dev).set_gemm_precision(precision)
+        return m, torch.optim.Adam(m.parameters(), lr=1e-4)
+
+    def timed(fn):
+        fn()                      # warmup pass (binds the engine, allocates workspaces)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / nbatch
+
+    m0, o0 = fresh()
+    m0.train()
+    T.train(m0, dev_batches[:1], dev, o0, crit)
+    adam = T.AdamBinding(m0, o0)
+    met = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
+    res = {"cnn_step_ms": timed(lambda: [T.train_step(m0, b["mfcc"], b["label"], b["poison_indicator"], adam, met)
+                                         for b in dev_batches])}
+    m1, o1 = fresh()
+    res["dropin_device_ms"] = timed(lambda: T.train(m1, dev_batches, dev, o1, crit))
+    m2, o2 = fresh()
+    res["dropin_loader_ms"] = timed(lambda: T.train(m2, loader, dev, o2, crit))
+    t0 = time.perf_counter()
+    for _ in loader:
+        pass
+    res["loader_only_ms"] = (time.perf_counter() - t0) * 1e3 / nbatch
+    res = {k: round(v, 4) for k, v in res.items()}
+    res["dropin_device_vs_cnn_step"] = round(res["dropin_device_ms"] / res["cnn_step_ms"], 4)
+    res["batches"], res["batch"], res["gemm_precision"] = nbatch, batch, precision
+    res["note"] = ("train() over a DataLoader of precomputed MFCC (the reference scripts' loop, badnets.py:146-160); "
+                   "dropin_device excludes the loader (batches already in HBM), dropin_loader includes collation "
+                   "and the pageable-memory H2D of each batch")
+    return res
 
 
 FEATURE_PHASES = ("stft_mel", "db_dct")
@@ -224,7 +322,9 @@ def main():
     ap.add_argument("--n-train", type=int, default=8192, help="resident training clips per GPU (the table is "
                     "replicated on every rank and holds n_train x world clips, so an epoch has the same number "
                     "of steps at every N)")
-    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps at the bench batch (0 = skip)")
+    ap.add_argument("--cpu-train", type=int, default=4096, help="CPU-baseline epoch size in clips (0 = skip)")
+    ap.add_argument("--dropin-batches", type=int, default=16, help="batches of the drop-in train() measurement "
+                    "(0 = skip; rank 0 at N = 1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
     ap.add_argument("--windows", type=int, default=5, help="equal windows of the timed steps (median reported)")
@@ -379,8 +479,13 @@ def main():
             per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "peak": pk, "frac": round(ach / pk, 4),
                               "ms": round(pms / pcnt, 4), "traffic": tb, "traffic_source": tsrc}
         cpu = None
-        if world == 1 and not args.no_cpu and args.cpu_steps > 0 and args.attack == "ultrasonic":
-            cpu = cpu_baseline(args.batch, cpu_threads(), args.cpu_steps)
+        if world == 1 and not args.no_cpu and args.cpu_train > 0 and args.attack == "ultrasonic":
+            cpu = cpu_baseline(args.batch, cpu_threads(), n_train=args.cpu_train)
+        dropin = None
+        if world == 1 and args.dropin_batches > 0:
+            dropin = dropin_bench(cfg, tr.waves, K, args.batch, args.dropin_batches, dev, args.gemm_precision)
+            cnn = sum(v[0] for k, v in wprof.result.items() if k not in FEATURE_PHASES) / max(args.profile_steps, 1)
+            dropin["resident_cnn_phase_ms_per_step"] = round(cnn, 4)
         value = n_utt / dt
         line = {
             "metric": "poisoned+clean utterances/sec/GPU; ASR & clean-acc parity vs reference",
@@ -407,6 +512,7 @@ def main():
             "roofline": roof,
             "step_roofline": step_roof,
             "cpu_baseline": cpu,
+            "dropin": dropin,
             "phases_ms_per_launch": phases_ms,
             "roofline_by_kernel": per_kernel,
             "train_metrics": {k: round(v, 4) if isinstance(v, float) else v for k, v in metrics.items()},

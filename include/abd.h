@@ -220,13 +220,15 @@ int abd_style_board_apply(const abd_style_board* board, const float* in, int64_t
 typedef struct abd_cnn abd_cnn;
 
 int abd_smallcnn_create(int H0, int W0, int num_classes, int max_batch, abd_cnn** net);
-/* GEMM precision of the conv2/conv3 forward and data-gradient products (BASELINE configs[2]:
- * "bf16, conv-as-GEMM on MFMA").  ABD_PREC_F32 (default): exact fp32 MFMA, the reference's
- * numerics.  ABD_PREC_BF16: operands rounded to bf16, fp32 accumulation (v_mfma_f32_32x32x16_bf16);
- * weight gradients, BatchNorm, fc layers and the loss stay fp32.  ABD_PREC_F32_SPLIT: fp32
+/* GEMM precision of the conv2/conv3 forward, data- and weight-gradient products.
+ * ABD_PREC_F32_SPLIT (the default of a new handle, the bench and the drop-in smallcnn): fp32
  * operands split exactly into three bf16 planes (x = x0 + x1 + x2) and multiplied as the six
  * terms with i + j <= 2 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- every term exact,
- * dropped terms <= ~2^-26 |a*b| (below one fp32 rounding), i.e. fp32-accurate GEMMs. */
+ * dropped terms <= ~2^-26 |a*b| (below one fp32 rounding), i.e. fp32-accurate GEMMs, parity-tested
+ * at the same 1e-4 fp32 tolerance as ABD_PREC_F32.  ABD_PREC_F32 (opt-in): fp32 MFMA
+ * (v_mfma_f32_32x32x2_f32), slower.  ABD_PREC_BF16 (BASELINE configs[2]/[4]: "bf16, conv-as-GEMM
+ * on MFMA"): operands rounded to bf16, fp32 accumulation; BatchNorm, fc layers and the loss stay
+ * fp32. */
 enum { ABD_PREC_F32 = 0, ABD_PREC_BF16 = 1, ABD_PREC_F32_SPLIT = 2 };
 int abd_smallcnn_set_precision(abd_cnn* net, int precision);
 void abd_smallcnn_destroy(abd_cnn* net);

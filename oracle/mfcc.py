@@ -153,9 +153,9 @@ def mfcc_core(wave2d: np.ndarray, sample_rate: int, n_mfcc: int, n_fft: int, hop
         fb = slaney_mel_fbanks(sample_rate, n_fft, n_mels)
     else:
         raise ValueError(f"unknown mel scale {mel!r}")
-    melspec = np.einsum("bft,fm->bmt", p, fb)
+    melspec = np.einsum("bft,fm->bmt", p, fb, optimize=True)
     db = amplitude_to_db(melspec, top_db=top_db)
-    return np.einsum("bmt,mc->bct", db, dct_ortho(n_mfcc, n_mels))
+    return np.einsum("bmt,mc->bct", db, dct_ortho(n_mfcc, n_mels), optimize=True)
 
 
 def mfcc_torchaudio(waveform, sample_rate: int, n_mfcc: int, n_fft: int, hop_length: int) -> np.ndarray:

@@ -24,7 +24,7 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$O/bench.json" 2> "$O/bench
 cat "$O/bench.json"
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 cd /tmp && export TMPDIR=/tmp
-CMD="python3 $R/bench.py --steps 10 --warmup 3 --profile-steps 1 --no-cpu"
+CMD="python3 $R/bench.py --steps 10 --warmup 3 --profile-steps 1 --no-cpu --dropin-batches 0"
 step kernel-trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt -f csv -- $CMD > "$O/kt.log" 2>&1 || { tail -20 "$O/kt.log"; exit 1; }
 [ "${SKIP_PMC:-0}" = 1 ] && exit 0

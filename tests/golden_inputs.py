@@ -136,6 +136,15 @@ CONV_CFGS = {
                     n_train=2048, n_test=512, epochs=8, clip_seed=101, init_seed=1234),
     "ultrasonic": dict(attack="ultrasonic", sr=44100, L=44100, n_fft=1103, hop=441, n_mfcc=40, K=35, lf=3072,
                        B=512, n_train=4096, n_test=1024, epochs=14, clip_seed=102, init_seed=1235),
+    # jingleback.py:127-197 (style 5 board, B = 256 hard-coded at :129-132), daba.py:142-219
+    # (librosa MFCC 32 x 40, fc 896, args.batch_size 256), flowmur.py:42-191 (clean-label, MFCC
+    # 2048/512 with 13 coefficients -> 32 x 13, fc 224, args.batch_size 256)
+    "jingleback": dict(attack="jingleback", sr=16000, L=16000, n_fft=400, hop=160, n_mfcc=40, K=10, lf=3072, B=256,
+                       n_train=2048, n_test=512, epochs=8, clip_seed=103, init_seed=1236),
+    "daba": dict(attack="daba", sr=16000, L=16000, n_fft=2048, hop=512, n_mfcc=40, K=10, lf=896, B=256,
+                 n_train=4096, n_test=1024, epochs=12, clip_seed=104, init_seed=1237),
+    "flowmur": dict(attack="flowmur", sr=16000, L=16000, n_fft=2048, hop=512, n_mfcc=13, K=10, lf=224, B=256,
+                    n_train=4096, n_test=1024, epochs=12, clip_seed=105, init_seed=1238, snr_db=30, Lt=8000),
 }
 
 
@@ -149,18 +158,49 @@ def ultrasonic_trigger_f32():
     return ultrasonic_gate(t[None].astype(np.float64) / 32768.0, 60, "mid", cont=False).astype(np.float32)
 
 
-def convergence_data(name):
-    """Clean / poisoned features exactly as badnets_poison_data (badnets.py:38-95) or
-    ultrasonic_poison_data (ultrasonic.py:40-124) builds them, from deterministic synthetic clips.
+def daba_trigger_int16():
+    """resources/DABA/trigger_pool/music0_0.wav (the fixture copy in daba_golden.npz)."""
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    return np.load(os.path.join(here, "golden", "daba_golden.npz"))["pool0"].copy()
 
-    Must run right after fix_random() (it draws the poisoned rows with the global ``random``).
-    Features come from oracle.torch_ref.mfcc, the torch-CPU restatement of torchaudio's T.MFCC."""
+
+def flowmur_trigger_f32(Lt=8000):
+    """The optimised trigger of the flowmur fixture, in place of sp_trigger300.npy (flowmur.py:67,
+    not in the reference): made by tests/golden/make_flowmur_conv_trigger.py the way the
+    reference's generate_trigger would (surrogate smallcnn + SNR-30 mix + MFCC + CE to label 2)."""
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    t = np.load(os.path.join(here, "golden", "flowmur_conv_trigger.npy"))
+    assert t.shape == (Lt,) and t.dtype == np.float32
+    return t
+
+
+def convergence_data(name):
+    """Clean / poisoned features exactly as the attack's poisoning step builds them, from
+    deterministic synthetic clips: badnets_poison_data (badnets.py:38-95), ultrasonic_poison_data
+    (ultrasonic.py:40-124), style_poison_data (jingleback.py:38-119, style 5), daba_poison_data's
+    injection + get_data (utils/daba_injection_tools.py:102-211, daba.py:55-82) and
+    flowmur_poison_data (flowmur.py:42-127).
+
+    Must run right after fix_random() (it draws the poisoned rows with the global ``random`` /
+    ``np.random``).  torchaudio features come from oracle.torch_ref.mfcc (the torch-CPU restatement
+    of T.MFCC), librosa's from oracle.mfcc.mfcc_librosa (float64, then ``.float()``), the style board
+    from oracle.effects.style5, pydub's overlay from oracle.triggers.
+    DABA's trigger / host SELECTION (certainty + influence, daba_selection_tools.py:154-160) is not
+    replayed here: its inputs are an untrained model's batch-1 forwards, pinned separately
+    (tests/golden/daba_golden.npz); the hosts are a random.sample of the non-target train clips and
+    the trigger is the pool's first clip, with the reference's variant-dB schedule."""
     import random
 
     import torch
     from abd_amd import synth
     from oracle import torch_ref
     c = CONV_CFGS[name]
+    if c["attack"] == "daba":
+        return _daba_convergence_data(c)
+    if c["attack"] == "flowmur":
+        return _flowmur_convergence_data(c)
     n = c["n_train"] + c["n_test"]
     waves, labels = synth.make_clips_np(n, c["sr"], c["L"], c["K"], seed=c["clip_seed"])
 
@@ -187,6 +227,16 @@ def convergence_data(name):
         bd_x[rows] = poison(bd_x[rows])
         bt_x = te_x.copy()
         bt_x[test_pois] = poison(bt_x[test_pois])
+    elif c["attack"] == "jingleback":
+        from oracle import effects as oe
+
+        def styled(w):   # pedalboard runs float32 (styles_trigger.py:51-53)
+            return oe.style5(w, c["sr"]).astype(np.float32)
+        bd_x = tr_x.copy()
+        srt = np.sort(rows)
+        bd_x[srt] = feats(styled(waves[:ntr][srt]))
+        bt_x = te_x.copy()
+        bt_x[test_pois] = feats(styled(waves[ntr:][test_pois]))
     else:
         trig = ultrasonic_trigger_f32()
         bd_x = tr_x.copy()
@@ -196,6 +246,82 @@ def convergence_data(name):
         bt_x[test_pois] = feats(waves[ntr:][test_pois] + trig)
     return dict(bd_x=bd_x, bd_y=bd_y.astype(np.int64), ind=ind, clean_x=te_x, clean_y=te_y.astype(np.int64),
                 bt_x=bt_x, bt_y=np.full(c["n_test"], 2, np.int64), bt_ind=test_pois.astype(np.int64))
+
+
+def _daba_convergence_data(c):
+    import random
+
+    from abd_amd import synth
+    from oracle import mfcc as om
+    from oracle import triggers as otr
+    n = c["n_train"] + c["n_test"]
+    waves, labels = synth.make_clips_np(n, c["sr"], c["L"], c["K"], seed=c["clip_seed"])
+    pcm = np.round(waves.astype(np.float64) * 32768.0).astype(np.int16)       # the wav files' samples
+    ntr, target = c["n_train"], 2                                              # 'up' = SCDv1-10 index 2
+    tr_y, te_y = labels[:ntr].copy(), labels[ntr:].copy()
+    hosts = [i for i in range(ntr) if tr_y[i] != target]
+    poison_num = round(c.get("rate", 0.1) * ntr)                               # daba_injection_tools.py:116-117
+    rows = sorted(random.sample(hosts, poison_num))
+    mean_db = otr.gen_trigger_variants_db(poison_num)                          # :136-137 (re-seeds random)
+    trig = daba_trigger_int16()
+
+    def feats(p16):   # soundfile -> librosa_MFCC(.., 40).T[np.newaxis] -> torch.tensor(..).float()
+        w = np.asarray(p16).astype(np.float64) / 32768.0       # (== om.mfcc_librosa per clip, batched)
+        out = [om.mfcc_core(w[s:s + 256], c["sr"], c["n_mfcc"], c["n_fft"], c["hop"], mel="slaney",
+                            pad_mode="constant") for s in range(0, len(w), 256)]
+        return np.transpose(np.concatenate(out), (0, 2, 1))[:, None].astype(np.float32)
+
+    tr_x, te_x = feats(pcm[:ntr]), feats(pcm[ntr:])
+    bd_x, bd_y = tr_x.copy(), tr_y.copy()
+    ind = np.zeros(ntr, np.int64)
+    bd_x[rows] = feats([otr.single_trigger_injection_db(pcm[r], trig, mean_db[k]) for k, r in enumerate(rows)])
+    bd_y[rows] = target
+    ind[rows] = 1
+    test_pois = te_y != target                                                 # :203-209 (po_db = -20)
+    bt_x = te_x.copy()
+    bt_x[test_pois] = feats([otr.single_trigger_injection_db(pcm[ntr + i], trig, -20)
+                             for i in np.nonzero(test_pois)[0]])
+    return dict(bd_x=bd_x, bd_y=bd_y.astype(np.int64), ind=ind, clean_x=te_x, clean_y=te_y.astype(np.int64),
+                bt_x=bt_x, bt_y=np.full(c["n_test"], target, np.int64), bt_ind=test_pois.astype(np.int64))
+
+
+def _flowmur_convergence_data(c):
+    import random
+
+    import torch
+    from abd_amd import synth
+    from oracle import torch_ref
+    n = c["n_train"] + c["n_test"]
+    waves, labels = synth.make_clips_np(n, c["sr"], c["L"], c["K"], seed=c["clip_seed"])
+    ntr, target, Lt = c["n_train"], 2, c["Lt"]
+    trw = torch.from_numpy(waves[:ntr].copy())[:, None]       # (N, 1, L) float32 like the reference
+    tew = torch.from_numpy(waves[ntr:].copy())[:, None]
+    tr_y, te_y = labels[:ntr].copy(), labels[ntr:].copy()
+    trigger = torch.from_numpy(flowmur_trigger_f32(Lt))[None]
+    tidx = np.where(tr_y == target)[0]                        # flowmur.py:74-76
+    poison_num = int(tidx.shape[0] * 0.1)
+    pidx = np.random.choice(tidx, poison_num, replace=False)
+    trigger_rms = torch.linalg.norm(trigger.clone(), dim=1)
+    for i in pidx:                                            # :78-85
+        wav_rms = torch.linalg.norm(trw[i].clone(), dim=1)
+        scale = torch.sqrt(torch.pow(wav_rms, 2) / torch.pow(trigger_rms, 2) * (10 ** (-c["snr_db"] / 10)))
+        pos = random.randint(0, trw.shape[2] - Lt)
+        trw[i][0][pos:pos + Lt] = trw[i][0][pos:pos + Lt] + scale * trigger[0]
+
+    def feats(w):     # MFCC(...).permute(0, 1, 3, 2) -> (N, 1, T, 13)
+        return torch_ref.mfcc(w[:, 0].contiguous(), c["sr"], c["n_mfcc"], c["n_fft"], c["hop"]).numpy()
+
+    bd_x = feats(trw)
+    ind = (tr_y == target).astype(np.int64)                   # :88-89 (every target clip counts)
+    clean_x = feats(tew)                                      # :93
+    keep = np.where(te_y != target)[0]                        # :95-99
+    bw = tew[keep].clone()
+    for i in range(bw.shape[0]):                              # :100-105
+        pos = random.randint(0, bw.shape[2] - Lt)
+        bw[i][0] = torch.cat([bw[i][0][:pos] / 2, (bw[i][0][pos:pos + Lt] + trigger[0]) / 2, bw[i][0][pos + Lt:] / 2])
+    bt_x = feats(bw)
+    return dict(bd_x=bd_x, bd_y=tr_y.astype(np.int64), ind=ind, clean_x=clean_x, clean_y=te_y.astype(np.int64),
+                bt_x=bt_x, bt_y=np.full(len(keep), target, np.int64), bt_ind=np.ones(len(keep), np.int64))
 
 
 def data_digest(d):

@@ -70,7 +70,7 @@ def test_whole_module_checkpoint_round_trip(tmp_path):
     from conftest import load_dropin_checkpoint
     loaded = load_dropin_checkpoint(path)
     assert isinstance(loaded, smallcnn) and loaded._engine is None and loaded._step == 0
-    assert loaded.gemm_precision == "f32" and not loaded.training
+    assert loaded.gemm_precision == "f32split" and not loaded.training
     a, b = m.state_dict(), loaded.state_dict()
     assert sorted(a) == sorted(b) and all(torch.equal(a[k], b[k]) for k in a)
 
@@ -141,3 +141,80 @@ def test_checkpoint_loads_as_reference_class_without_abd(tmp_path, K, lf, H, W):
         exp_p = t(x)
     assert torch.allclose(ys["y"], exp, rtol=1e-5, atol=1e-5)
     assert torch.allclose(ys["yp"], exp_p, rtol=1e-5, atol=1e-5)
+
+
+def _pickle_ops(path):
+    import pickletools
+    import zipfile
+    z = zipfile.ZipFile(path)
+    data = z.read([n for n in z.namelist() if n.endswith("data.pkl")][0])
+    return [(op.name, arg) for op, arg, _ in pickletools.genops(data)
+            if op.name in ("GLOBAL", "STACK_GLOBAL", "NEWOBJ", "REDUCE", "BUILD")]
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "utils")), reason="reference checkout not present")
+def test_checkpoint_opcodes_equal_reference_torch_save(tmp_path):
+    """the stream is the reference's own torch.save(model) (utils/training_tools.py:49) --
+    GLOBAL utils.models smallcnn + NEWOBJ, no import_module / getattr REDUCE calls -- opcode for opcode."""
+    m, path = _write_checkpoint(tmp_path, 10, 896)
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    try:
+        import utils.models as ref_models
+    finally:
+        sys.path.remove(REF)
+    ref = ref_models.smallcnn(10, 896)
+    ref.load_state_dict(m.state_dict())
+    ref.eval()
+    rpath = str(tmp_path / "ref.pt")
+    torch.save(ref, rpath)
+    ours, theirs = _pickle_ops(path), _pickle_ops(rpath)
+    assert ours[0] == ("GLOBAL", "utils.models smallcnn") and ours[1][0] == "NEWOBJ"
+    assert not any(a in ("importlib import_module", "builtins getattr") for _, a in ours)
+    assert ours == theirs
+
+
+_SAFE_CONSUMER = r"""
+import sys, json, collections
+sys.dont_write_bytecode = True
+sys.path[:] = [p for p in sys.path if p and 'repo' not in p]
+sys.path.insert(0, {ref!r})
+import torch, torch.nn as nn
+import utils.models as rm
+allow = [rm.smallcnn, nn.Conv2d, nn.BatchNorm2d, nn.MaxPool2d, nn.Dropout, nn.Flatten, nn.Linear, nn.Softmax,
+         collections.OrderedDict, set]
+with torch.serialization.safe_globals(allow):
+    m = torch.load({path!r}, map_location='cpu')            # weights_only=True: torch>=2.6 default
+m.eval()
+x = torch.load({xpath!r}, weights_only=True)
+with torch.no_grad():
+    torch.save(m(x), {ypath!r})
+print(json.dumps({{"cls": type(m).__module__ + "." + type(m).__name__,
+                   "abd_loaded": any(k.startswith('abd_amd') for k in sys.modules)}}))
+"""
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "utils")), reason="reference checkout not present")
+def test_checkpoint_loads_weights_only_with_reference_allowlist(tmp_path):
+    """torch.load's weights_only=True default accepts the checkpoint once the consumer
+    allowlists the reference's classes -- exactly what it needs for the reference's own pickle."""
+    import json
+    import subprocess
+    m, path = _write_checkpoint(tmp_path, 10, 896)
+    torch.manual_seed(4)
+    x = torch.randn(3, 1, 32, 40) * 20
+    xpath, ypath = str(tmp_path / "x.pt"), str(tmp_path / "y.pt")
+    torch.save(x, xpath)
+    code = _SAFE_CONSUMER.format(ref=REF, path=path, xpath=xpath, ypath=ypath)
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    env["PYTHONDONTWRITEBYTECODE"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=str(tmp_path),
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"cls": "utils.models.smallcnn", "abd_loaded": False}, out
+    t = torch_ref.SmallCNN(10, 896)
+    t.load_state_dict(m.state_dict(), strict=True)
+    t.eval()
+    with torch.no_grad():
+        assert torch.allclose(torch.load(ypath, weights_only=True), t(x), rtol=1e-5, atol=1e-5)

@@ -168,3 +168,26 @@ def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name, pre
     assert tr[-1, 0] < tr[0, 0]                                  # training converges
     assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5, (te[-1], rte[-1])   # clean accuracy (pp)
     assert abs(te[-1, 1] - rte[-1, 1]) <= 0.5, (te[-1], rte[-1])   # attack success rate (pp)
+
+
+# bf16 conv GEMMs (BASELINE configs[2] jingleback and configs[4] flowmur name bf16; badnets shares
+# jingleback's 101 x 40 geometry).  The per-epoch losses of a bf16 run are not expected to track
+# the fp32 reference at 1e-4 (operands rounded to 8 significand bits); the north_star's claim for
+# them is the final clean accuracy / ASR within +-0.5 pp of the reference's -- asserted as is, in
+# both dropout modes, with the loss gaps printed for DESIGN.md.
+BF16_CFGS = [n for n in ("badnets", "jingleback", "flowmur") if n in CONV_CFGS]
+
+
+@pytest.mark.parametrize("source", ["torch_cpu", "device"])
+@pytest.mark.parametrize("name", BF16_CFGS)
+def test_bf16_final_metrics_within_half_point(dev, conv_ref, name, source):
+    tr, te, _, _ = eval_model(name, dev, source, conv_ref, "bf16")
+    rtr, rte = conv_ref[f"{name}_train"], conv_ref[f"{name}_test"]
+    rel = lambda a, b: np.abs(a - b) / np.maximum(np.abs(b), 1e-12)  # noqa: E731
+    print(f"\n{name} [bf16, {source}] per epoch: |train loss - ref| / ref, clean acc / ASR (GPU vs reference)")
+    for e in range(len(rtr)):
+        print(f"  epoch {e + 1:2d}: {rel(tr[e, 0], rtr[e, 0]):.1e}  {te[e, 0]:.3f}/{te[e, 1]:.3f} vs "
+              f"{rte[e, 0]:.3f}/{rte[e, 1]:.3f}")
+    assert tr[-1, 0] < tr[0, 0]
+    assert abs(te[-1, 0] - rte[-1, 0]) <= 0.5, ("clean accuracy (pp)", te[-1], rte[-1])
+    assert abs(te[-1, 1] - rte[-1, 1]) <= 0.5, ("attack success rate (pp)", te[-1], rte[-1])

@@ -216,3 +216,22 @@ def test_daba_poison_data_end_to_end(dev, dg, tmp_path):
         got, _ = read_wav_int16(out + "/poison/train/up/" + f)
         cands = [ot.single_trigger_injection_db(c, tclip, variants[k]) for c in clean.values() if c.size == got.size]
         assert any(np.array_equal(got, c) for c in cands)
+
+
+def test_notebook_overlay_pin_on_device(dev):
+    """test.ipynb cells 30-32 (the reference's only held values for pydub's int16 overlay):
+    AudioSegment.overlay(song, song) -> [-16 -22 -22 ... 26 20 32], through libabd's
+    abd_pydub_overlay_i16 (triggers.single_trigger_injection_db, gain 0 dB) and the ragged kernel
+    with soundfile's int16 / 32768 fused (cell 30's [-0.00024414 ... 0.00048828])."""
+    from abd_amd import triggers as TR
+    from test_oracle_golden import notebook_test_wav, NB32_HEAD, NB32_TAIL, NB30_HEAD, NB30_TAIL
+    x = notebook_test_wav()
+    o = TR.single_trigger_injection_db(x, x, "keep")
+    np.testing.assert_array_equal(o[:3], NB32_HEAD)
+    np.testing.assert_array_equal(o[-3:], NB32_TAIL)
+    np.testing.assert_array_equal(o, ot.pydub_overlay(x, x))
+    zero = np.zeros_like(x)
+    buf, lens, Lmax = D._pack_ragged([x], dev)
+    f = D.overlay_to_float(buf, lens, torch.tensor(zero, device=dev), D.gain_factors([0.0], dev), Lmax).cpu().numpy()[0]
+    np.testing.assert_array_equal(np.round(f[:3].astype(np.float64), 8), NB30_HEAD)
+    np.testing.assert_array_equal(np.round(f[-3:].astype(np.float64), 8), NB30_TAIL)

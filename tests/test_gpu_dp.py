@@ -122,7 +122,9 @@ def _equiv_worker(rank, world, port, q):
         waves, labels = synth.make_clips_torch(256, cfg.sample_rate, cfg.length, K, seed=35, device=dev)
 
         def run(world_, rank_, pg_world):
-            torch.manual_seed(35)
+            # rank 1 seeded differently (the seed + rank pattern): parameters, BN buffers AND the
+            # dropout seed come from rank 0, so the run still equals the 1-rank run
+            torch.manual_seed(35 + 1000 * rank_)
             model = smallcnn(K, cfg.linear_features).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
             tr = ResidentTrainer(cfg, waves, labels, model, opt, B // world_, seed=35, rank=rank_, world=world_,

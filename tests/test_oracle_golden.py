@@ -195,3 +195,59 @@ def test_flowmur_oracle_matches_autograd_golden():
                for e in range(c["epochs"])]
     traj = of.optimise(m, batches, c["Lt"], c["epochs"])
     assert np.abs(traj - g["traj"]).max() < 1e-10
+
+
+# test.ipynb known answers (the notebook's printed outputs; SURVEY §4 items 2 and cells 29-32)
+NB12_HEAD, NB12_TAIL = [0.0000, 0.0471, -0.0932], [-0.2744, 0.1865, -0.0942]   # cell 12 (torch 4-digit print)
+NB30_HEAD, NB30_TAIL = [-0.00024414, -0.00033569, -0.00033569], [0.00039673, 0.00030518, 0.00048828]  # cell 30
+NB29_HEAD, NB29_TAIL = [-0.0002, -0.0003, -0.0003], [0.0004, 0.0003, 0.0005]   # cell 29 (torchaudio.load)
+NB32_HEAD, NB32_TAIL = [-16, -22, -22], [26, 20, 32]                             # cell 32: overlay(song, song)
+
+
+def notebook_test_wav():
+    """A 16,000-sample int16 clip whose first and last three samples are test.wav's as printed in
+    cell 30 (soundfile float = int16 / 32768: -8, -11, -11 ... 13, 10, 16); test.wav itself is not
+    in the reference, so the interior is synthetic -- with saturating samples, which overlay clamps."""
+    r = np.random.Generator(np.random.PCG64(30))
+    x = r.integers(-20000, 20000, 16000).astype(np.int16)
+    x[100:110] = 32767
+    x[200:210] = -32768
+    x[:3] = np.round(np.array(NB30_HEAD) * 32768).astype(np.int16)
+    x[-3:] = np.round(np.array(NB30_TAIL) * 32768).astype(np.int16)
+    return x
+
+
+def test_notebook_cell12_loader_normalisation(wavs):
+    """cell 10-12: torchaudio.load(trigger.wav) + torchaudio.load(ante.wav), printed to 4 digits:
+    [0.0000, 0.0471, -0.0932, ..., -0.2744, 0.1865, -0.0942] -- int16 / 32768 in float32."""
+    from abd_amd import io as aio
+    import os
+    import tempfile
+    s = (wavs["ultrasonic_trigger_int16"].astype(np.float32) / 32768.0
+         + wavs["ante_int16"].astype(np.float32) / 32768.0)
+    np.testing.assert_array_equal(np.round(s[:3].astype(np.float64), 4), NB12_HEAD)
+    np.testing.assert_array_equal(np.round(s[-3:].astype(np.float64), 4), NB12_TAIL)
+    # the package's own wav loader (io.read_wav) gives the same sum
+    with tempfile.TemporaryDirectory() as d:
+        pa, pb = os.path.join(d, "a.wav"), os.path.join(d, "b.wav")
+        aio.write_wav_int16(pa, wavs["ultrasonic_trigger_int16"], 44100)
+        aio.write_wav_int16(pb, wavs["ante_int16"], 44100)
+        (a, sra), (b, srb) = aio.read_wav(pa), aio.read_wav(pb)
+    assert sra == srb == 44100 and a.dtype == np.float32
+    np.testing.assert_array_equal(a + b, s)
+
+
+def test_notebook_cells29_32_soundfile_and_overlay():
+    """cells 29/30: the clip read by torchaudio (4 decimals) and soundfile (8 decimals);
+    cells 31/32: AudioSegment.overlay(song, song) printed as int16 [-16 -22 -22 ... 26 20 32]."""
+    x = notebook_test_wav()
+    f = x.astype(np.float64) / 32768.0
+    np.testing.assert_array_equal(np.round(f[:3], 8), NB30_HEAD)     # numpy's 8-decimal print
+    np.testing.assert_array_equal(np.round(f[-3:], 8), NB30_TAIL)
+    np.testing.assert_array_equal(np.round(f[:3].astype(np.float32).astype(np.float64), 4), NB29_HEAD)
+    np.testing.assert_array_equal(np.round(f[-3:].astype(np.float32).astype(np.float64), 4), NB29_TAIL)
+    o = otr.pydub_overlay(x, x)
+    np.testing.assert_array_equal(o[:3], NB32_HEAD)
+    np.testing.assert_array_equal(o[-3:], NB32_TAIL)
+    assert o[105] == 32767 and o[205] == -32768      # saturating add (audioop.add)
+    np.testing.assert_array_equal(otr.single_trigger_injection_db(x, x, "keep"), o)
