@@ -52,7 +52,7 @@ constexpr bool kGatherV4 = true;
 
 struct MfccDev {
   int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
-  int ablate;  // diagnostics only (ABD_STFT_ABLATE): 1 skip sample loads, 2 skip FFTs, 4 skip mel
+  int ablate;  // diagnostics only (0 in the library; measurement builds set it): 1 skip sample loads, 2 skip FFTs, 4 skip mel
   int64_t L;
   float top_db;
   int radix[16], ns[16];
@@ -1902,10 +1902,6 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
 int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
                   const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
                   hipStream_t s) {
-  static const int nblk = getenv("ABD_STFT_BLOCKS") ? atoi(getenv("ABD_STFT_BLOCKS")) : 8;  // A/B knob
-  if (d.M == 2304 && d.N == 1103 && d.bluestein && nblk == 7)
-    return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true, 7>(d, wave, row_stride, rows, batch, ij, rowscale,
-                                                                          ws_db, ws_max, queue, s);
   if (d.M == 2304 && d.N == 1103 && d.bluestein)
     return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
                                                        queue, s);
@@ -2045,12 +2041,14 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.top_db = top_db;
   const int P = (d.T + 1) / 2;
   const FastPlan* fp = find_fast(M, N, blue ? 1 : 0);
-  if (fp != nullptr && getenv("ABD_GENERIC_FFT") == nullptr) {
+  // ABD_GENERIC_FFT: every MFCC stage on its generic kernel (runtime-radix STFT, LDS mel, VALU DCT),
+  // the fallbacks of geometries without a specialised plan (tests/test_gpu_mfcc.py runs both)
+  const bool generic = getenv("ABD_GENERIC_FFT") != nullptr;
+  if (fp != nullptr && !generic) {
     d.ppb = fp->pp;  // fixed pairs per work item (compile-time in the fast kernel)
     d.chunks = (P + d.ppb - 1) / d.ppb;
     d.fast = 1;
-    const char* ab = getenv("ABD_STFT_ABLATE");
-    d.ablate = ab ? atoi(ab) : 0;
+    d.ablate = 0;
   } else {
     int ppb_max = std::max(1, kMaxComplexPerBlock / M);
     int chunks = (P + ppb_max - 1) / ppb_max;
@@ -2273,7 +2271,7 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
       dct[(size_t)m * n_mfcc + c] = (float)v;
     }
   // B fragments of db_dct_mfma_kernel: [s][q][tile][col] -> float4 over j of dct[16 s + 4 q + j][16 tile + col]
-  d.dct_tiles = (n_mels % 16 == 0 && n_mfcc <= 48 && getenv("ABD_DCT_NOMFMA") == nullptr) ? (n_mfcc + 15) / 16 : 0;
+  d.dct_tiles = (n_mels % 16 == 0 && n_mfcc <= 48 && !generic) ? (n_mfcc + 15) / 16 : 0;
   std::vector<float4> dfrag;
   if (d.dct_tiles > 0)
     for (int sg = 0; sg < n_mels / 16; ++sg)
@@ -2384,7 +2382,7 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.vhat4 = reinterpret_cast<const float4*>(b + off_vh4);
   d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
   d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
-  d.mel3_w = mw3.empty() || getenv("ABD_MEL_GENERIC") ? nullptr : reinterpret_cast<const float*>(b + off_w3);
+  d.mel3_w = mw3.empty() || generic ? nullptr : reinterpret_cast<const float*>(b + off_w3);
   d.bin_mel = reinterpret_cast<const int2*>(b + off_bm);
   d.bin_w = reinterpret_cast<const float2*>(b + off_bw);
   *plan = pl;
@@ -2499,8 +2497,7 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
     else if (d.dct_tiles == 2) db_dct_mfma_kernel<2><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
     else db_dct_mfma_kernel<3><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
   } else if (d.n_mfcc % 4 == 0 && dct_lds <= 64 * 1024 &&
-      (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
-      getenv("ABD_DCT_GENERIC") == nullptr) {
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && d.fast) {
     db_dct_lds_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT2 - 1) / kTT2)), dim3(kThreads), dct_lds, s>>>(
         d, ws_db, ws_max, ij, out);
   } else {

@@ -1180,27 +1180,11 @@ __device__ __forceinline__ void bn_bwd_derived_finish(int c, double s1, double s
   }
 }
 
-__global__ void __launch_bounds__(kT) bn_bwd_derived_kernel(const float* W, const float* G, const float* db, int Cout,
-                                                            int Cin, const float* gamma, const float* beta,
-                                                            const float4* coef, double count, float* dgamma,
-                                                            float* dbeta, BCoef* bcoef, double* sums) {
-  const int c = blockIdx.x;
-  const double b = (double)beta[c];
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < Cout * 4; i += kT) {
-    const int n = i >> 2, t = i & 3;
-    const int64_t e = ((int64_t)n * Cin + c) * 4 + t;
-    const double w = (double)W[e], d = (double)db[n];
-    s1 = fma(w, d, s1);
-    s2 = fma(w, fma(-b, d, (double)G[e]), s2);
-  }
-  bn_bwd_derived_finish(c, s1, s2, Cin, gamma, coef, count, dgamma, dbeta, bcoef, sums);
-}
-
 // The next BatchNorm's derivation fused into the conv weight gradient's last slab reduction
 // (slab_reduce_kernel with conv_cin = Cin): block c reduces the Cout * 4 entries of input channel c
 // (the same ordered_sum, so the gradient is bit-identical), stores them, and contracts them with the
-// conv weights as bn_bwd_derived_kernel does.  db (the conv bias gradient) is final before this launch.
+// conv weights: sum_(n,t) W[n,c,t] db[n] and sum W[n,c,t] (G[n,c,t] - beta_c db[n]).
+// db (the conv bias gradient) is final before this launch.
 struct DeriveArgs {
   const float4* fold;  // the weight gradient's source is folded (unfold_wgrad)
   const float* W;
@@ -1735,213 +1719,6 @@ __global__ void __launch_bounds__(kT, ABD_NT_MINW) gemm_nt_kernel(NTArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ bf16 MFMA variant (opt-in)
-// abd_smallcnn_set_precision(net, ABD_PREC_BF16) routes the conv2/conv3 forward and data-gradient
-// GEMMs (the MFMA-bound bulk of the step, BASELINE configs[2] "bf16, conv-as-GEMM on MFMA") through
-// v_mfma_f32_32x32x16_bf16: operands are rounded to bf16 (RNE) when staged into LDS, products are
-// accumulated in fp32, activations stay fp32 in HBM.  16x the fp32 MFMA rate; parity then holds
-// to bf16 tolerances, so the fp32 path stays the default.
-// Tile: 128 rows x NB columns, K chunks of KB channels of one tap; LDS rows of KB + 8 bf16
-// (KB = 64: 144-B rows, so every 16-lane group of a ds_read_b128 hits 16 distinct 4-bank
-// groups); wave w owns rows 32w..32w+31 x all NB columns (NB / 32 accumulators).
-
-// NP = 3 (ABD_PREC_F32_SPLIT): each fp32 operand x is staged as three bf16 planes x0 + x1 + x2 == x
-// exactly (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1: 8 + 8 + 8 significand bits), and the
-// product is accumulated from the six terms with i + j <= 2 (a2*b0, a0*b2, a1*b1, a1*b0, a0*b1,
-// a0*b0, small first).  Each term is exact in fp32 (8 x 8 bits); the dropped a1*b2 + a2*b1 + a2*b2
-// are <= ~2^-26 of |a*b|, below the 2^-24 rounding of one fp32 fma, so the GEMM carries fp32
-// accuracy at 6 x 32 MFMA cycles per 16-deep k-step instead of 8 x 64 for v_mfma_f32_32x32x2_f32.
-// MI = 32-row m-tiles per wave (block rows 128 * MI): MI = 2 halves the LDS reads per MFMA
-// (2 A + 2 B fragments per plane feed 4 accumulators), which the 3-plane split is bound by.
-// PD = 2: operand loads run two K chunks ahead (two register sets): the first tap of a chunk
-// streams x1 from HBM (~2 us latency), which one chunk of MFMAs (24 x 32 cycles) cannot cover.
-template <int NB, int EPI, int KB, int NP = 1, int MI = 1, int PD = 1>
-__global__ void __launch_bounds__(kT) gemm_nt_bf16_kernel(NTArgs a) {
-  static_assert(NP == 1 || NP == 3, "1 (bf16) or 3 (exact fp32 split) planes");
-  constexpr int BM = kBM * MI, LD = KB + 8, Q = KB / 4;  // Q float4 per row
-  constexpr int RPT = BM * Q / kT, BPT = NB * Q / kT, NJ = NB / 32;
-  static_assert(RPT >= 1 && BPT >= 1 && (BM * Q) % kT == 0 && (NB * Q) % kT == 0, "tile / thread mismatch");
-  __shared__ __attribute__((aligned(16))) __bf16 As[NP][BM * LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][NB * LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * NB;
-  const int q = tid % Q, r0 = tid / Q;
-  constexpr int RSTEP = kT / Q;
-  // Operands through buffer loads: A's descriptor starts at the block's first image, so each row
-  // is a 32-bit byte offset; a tap outside the source grid (or a row past M) loads from kOOB, which
-  // the descriptor's range check turns into zeros.  Per chunk: one add + one select per row.
-  constexpr uint32_t kOOB = 0x80000000u;
-  const int HoWo = a.Ho * a.Wo;
-  const int b0 = m0 / HoWo;
-  const int64_t img = (int64_t)a.Hs * a.Ws * a.Cs;
-  const int64_t abytes = (int64_t)((a.M + HoWo - 1) / HoWo - b0) * img * 4;
-  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.src + b0 * img), 0, (int)(abytes < 0x7ffffff0 ? abytes : 0x7ffffff0), 0x00020000);
-  const int64_t bbytes = (int64_t)a.N * a.ldb * 4;
-  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.Bw), 0, (int)(bbytes < 0x7ffffff0 ? bbytes : 0x7ffffff0), 0x00020000);
-  uint32_t roff[RPT], tmask[RPT], boff[BPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int m = m0 + r0 + RSTEP * i;
-    const bool rok = m < a.M;
-    const int mm = rok ? m : m0;
-    const int rb = mm / HoWo;
-    const int rem = mm - rb * HoWo;
-    const int rh = rem / a.Wo, rw = rem - rh * a.Wo;
-    roff[i] = (uint32_t)(((((int64_t)(rb - b0) * a.Hs + rh) * a.Ws + rw) * a.Cs + 4 * q) * 4);
-    uint32_t mk = 0;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int hs = rh + a.dh[t], ws = rw + a.dw[t];
-      if (t < a.taps && rok && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
-    }
-    tmask[i] = mk;
-  }
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    const int n = n0 + r0 + RSTEP * j;
-    boff[j] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + 4 * q) * 4) : kOOB;
-  }
-  const int cpt = a.Cs / KB;
-  const int nch = a.taps * cpt;
-  float4 ras[PD][RPT], rbs[PD][BPT];
-  auto load = [&](int ch, float4* ra, float4* rbv) {
-    const int t = ch / cpt;
-    const int c0 = (ch - t * cpt) * KB;
-    const uint32_t adelta = (uint32_t)(((a.dh[t] * a.Ws + a.dw[t]) * a.Cs + c0) * 4);
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const uint32_t off = (tmask[i] >> t) & 1u ? roff[i] + adelta : kOOB;
-      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
-    }
-    const uint32_t bdelta = (uint32_t)((t * a.Cs + c0) * 4);
-#pragma unroll
-    for (int j = 0; j < BPT; ++j)
-      rbv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)(boff[j] + bdelta), 0, 0));
-  };
-  // stage one float4 as NP bf16x4 planes, pstride elements apart.  Pairs: one v_cvt_pk_bf16_f32
-  // (RNE), the two bf16 widened back by bit moves, one v_pk_add_f32 for the exact residual.
-  auto put = [](__bf16* p0, int pstride, float4 v) {
-    f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
-#pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      uint32_t u[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const bf16x2 r = __builtin_convertvector(x[h], bf16x2);
-        u[h] = __builtin_bit_cast(uint32_t, r);
-        if (pl + 1 < NP) {
-          const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
-          x[h] -= back;  // exact: x - rne(x) fits in fp32
-        }
-      }
-      *reinterpret_cast<uint2*>(p0 + pl * pstride) = make_uint2(u[0], u[1]);
-    }
-  };
-  f32x16 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  // one K chunk: stage register set `slot` into LDS, refill it PD chunks ahead, MFMAs
-  auto chunk = [&](int ch, int slot) {
-    float4* ra = ras[slot];
-    float4* rbv = rbs[slot];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) put(&As[0][(r0 + RSTEP * i) * LD + 4 * q], BM * LD, ra[i]);
-#pragma unroll
-    for (int j = 0; j < BPT; ++j) put(&Bs[0][(r0 + RSTEP * j) * LD + 4 * q], NB * LD, rbv[j]);
-    __syncthreads();
-    if (ch + PD < nch) load(ch + PD, ra, rbv);
-    const int aoff = (wave * 32 * MI + (lane & 31)) * LD + 8 * (lane >> 5);
-    const int boff = (lane & 31) * LD + 8 * (lane >> 5);
-#pragma unroll
-    for (int ks = 0; ks < KB; ks += 16) {
-      bf16x8 av[MI][NP];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int pl = 0; pl < NP; ++pl) av[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl][aoff + i * 32 * LD + ks]);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        bf16x8 bv[NP];
-#pragma unroll
-        for (int pl = 0; pl < NP; ++pl) bv[pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl][boff + j * 32 * LD + ks]);
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          if constexpr (NP == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bv[0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bv[1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bv[0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[1], acc[i][j], 0, 0, 0);
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bv[0], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();
-  };
-#pragma unroll
-  for (int sl = 0; sl < PD; ++sl)
-    if (sl < nch) load(sl, ras[sl], rbs[sl]);
-  for (int ch = 0; ch < nch; ch += PD) {
-#pragma unroll
-    for (int sl = 0; sl < PD; ++sl)
-      if (ch + sl < nch) chunk(ch + sl, sl);
-  }
-  // epilogue (same maps as the fp32 kernel): row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31
-  float st[NJ][2];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    st[j][0] = st[j][1] = 0.0f;
-    const int col = n0 + j * 32 + (lane & 31);
-    const bool cok = col < a.N;
-    float bias = 0.0f;
-    if constexpr (EPI == EPI_CONV) bias = cok ? a.bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wave * 32 * MI + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m >= a.M || !cok) continue;
-      float v = acc[i][j][r];
-      if constexpr (EPI == EPI_CONV) {
-        v = fmaxf(v + bias, 0.0f);
-        st[j][0] += v;
-        st[j][1] = fmaf(v, v, st[j][1]);
-      }
-      a.out[(int64_t)m * a.ldc + col] = v;
-    }
-  }
-  if constexpr (EPI == EPI_CONV) {
-    if (a.part == nullptr) return;
-    __shared__ float red[4 * NB * 2];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
-      const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
-      if (lane < 32) {
-        red[(wave * NB + j * 32 + lane) * 2 + 0] = s0;
-        red[(wave * NB + j * 32 + lane) * 2 + 1] = s1;
-      }
-    }
-    __syncthreads();
-    if (tid < NB && n0 + tid < a.N) {
-      float s0 = 0.0f, s1 = 0.0f;
-      for (int w = 0; w < 4; ++w) {
-        s0 += red[(w * NB + tid) * 2 + 0];
-        s1 += red[(w * NB + tid) * 2 + 1];
-      }
-      a.part[((int64_t)0 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s0;
-      a.part[((int64_t)1 * a.N + n0 + tid) * a.nblk + blockIdx.x] = s1;
-    }
-  }
-}
-
 // Weight-stationary 2x2 conv GEMM, 3-plane split (ABD_PREC_F32_SPLIT), Cs = N = 64, 4 taps, K = 256:
 // conv2 forward (EPI_CONV: bias + ReLU + BN2 statistics) and data gradient (EPI_STORE).
 //   * the whole weight operand (64 x 256, three exact bf16 planes, 101 KB with conflict-free
@@ -2246,6 +2023,12 @@ __global__ void __launch_bounds__(WPB * 64, 1) conv_ws_split_kernel(NTArgs a) {
 #define ABD_DMA_TRIM 1
 #endif
 constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31 + 3 + 14 + Ws + 1)
+#ifndef ABD_DMA_ABL  // ablation bits (measurement builds only; results wrong): 1 no epilogue stores,
+#define ABD_DMA_ABL 0  // 2 no DMA waits, 4 no DMA, 8 no A split
+#endif
+#ifndef ABD_DMA_SPREAD  // A/B: the DMA refill spread over taps 1-3 (1) or issued at tap 1 (0)
+#define ABD_DMA_SPREAD 0
+#endif
 template <int EPI, int NP, int NJ = 2>
 __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   constexpr int CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
@@ -2299,23 +2082,25 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
     bias[j] = 0.0f;
     if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
   }
-  float* sw = stage[wave];
-  __attribute__((address_space(3))) void* swl = (__attribute__((address_space(3))) void*)sw;
+  // the wave index as a scalar: the DMA's LDS base (M0) is then plain scalar arithmetic, not a
+  // v_readfirstlane of a per-lane address before every DMA instruction
+  float* sw = stage[__builtin_amdgcn_readfirstlane(wave)];
   // DMA of channel group cg for the span starting at source position p0: instruction i, lane l ->
   // position 16 i + l / 4, LDS slot l % 4 holds global chunk (l % 4) ^ ((pos >> 2) & 3)
   // only the 16-position blocks the tile reads (need: wave-uniform; typically 48 of the 64 slots)
+  auto dma1 = [&](int p0, int cg, int need, int i) {
+    if (ABD_DMA_ABL & 4) return;
+    if (i > 0 && 16 * i >= need) return;
+    const int pos = 16 * i + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
+    const uint32_t off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (__attribute__((address_space(3))) void*)(sw + i * 256), 16,
+                                             (int)off, 0, 0, 0);
+  };
   auto dma = [&](int p0, int cg, int need) {
 #pragma unroll
-    for (int i = 0; i < kDmaSpan / 16; ++i) {
-      if (i > 0 && 16 * i >= need) break;
-      const int pos = 16 * i + (lane >> 2);
-      const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
-      const uint32_t off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (__attribute__((address_space(3))) void*)(sw + i * 256), 16,
-                                               (int)off, 0, 0, 0);
-    }
+    for (int i = 0; i < kDmaSpan / 16; ++i) dma1(p0, cg, need, i);
   };
-  (void)swl;
   const int ntiles = (r_hi - r_lo + 31) / 32;
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
       a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
@@ -2385,7 +2170,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
       // order).  The count must equal the stores per tile exactly: a larger one lets the DMA
       // of group 0 still be in flight (NJ = 1 issues 16 stores: vmcnt(32) would never wait).
       static_assert(NJ == 1 || NJ == 2, "epilogue store count per tile is 16 * NJ");
-      if (cg == 0 && tile > 0) {
+      if (ABD_DMA_ABL & 6) {
+      } else if (cg == 0 && tile > 0) {
         if constexpr (NJ == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       } else {
@@ -2410,6 +2196,20 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
           // little) before the buffer is refilled: with group cg + 1, or after the last group with
           // the next tile's group 0
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if (ABD_DMA_SPREAD) {
+          // the refill's instructions spread over taps 1-3 (instruction i at tap 1 + i, the 4th with
+          // the 3rd): each tap's MFMAs carry one DMA issue instead of tap 1 carrying all of them
+          if (t >= 1) {
+            if (cg + 1 < G) {
+              dma1(p0, cg + 1, need, t - 1);
+              if (t == 3) dma1(p0, cg + 1, need, 3);
+            } else if (more) {
+              dma1(p0n, 0, needn, t - 1);
+              if (t == 3) dma1(p0n, 0, needn, 3);
+            }
+          }
+        } else if (t == 1) {
           if (cg + 1 < G) dma(p0, cg + 1, need);
           else if (more) dma(p0n, 0, needn);
         }
@@ -2417,7 +2217,12 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
         // next step's B fragments (past the tile's last step: the next tile's first)
         load_b(((s + 1) % (4 * G)) / 4, (s + 1) % 4, bvs[(s + 1) & 1]);
         bf16x8 av[NP];
-        planes_x8<NP>(__builtin_bit_cast(float4, raw[t][0]), __builtin_bit_cast(float4, raw[t][1]), av);
+        if (ABD_DMA_ABL & 8) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) av[q] = __builtin_bit_cast(bf16x8, q == 1 ? raw[t][1] : raw[t][0]);
+        } else {
+          planes_x8<NP>(__builtin_bit_cast(float4, raw[t][0]), __builtin_bit_cast(float4, raw[t][1]), av);
+        }
         bf16x8 (&bv)[NJ][NP] = bvs[s & 1];
 #pragma unroll
         for (int term = 0; term < Terms<NP>::n; ++term)
@@ -2442,6 +2247,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
           st[j][0] += vs;
           st[j][1] = fmaf(vs, vs, st[j][1]);
         }
+        if ((ABD_DMA_ABL & 1) && __builtin_bit_cast(uint32_t, v) != 0x7fc00001u) continue;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
       }
     }
@@ -2468,189 +2274,6 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   }
 }
 
-// Halo-tiled 2x2 conv GEMM, 3-plane split (ABD_PREC_F32_SPLIT), Cs = N = 64: conv2 forward and
-// data gradient.  The 128 output rows of a block (consecutive m, possibly across two images) read
-// source positions inside one contiguous span of whole source rows [s_lo, s_hi); per 32-channel
-// half, that span is loaded once (coalesced 128-B runs, buffer range check past s_hi) and staged
-// once as three exact bf16 planes, and all four taps read their A fragments from it -- instead of
-// four im2col loads + four plane splits of every source element.  B (the tap's 32 x 64 weight
-// slice) is staged per tap as in gemm_nt_bf16_kernel.  A tap outside the source grid reads the
-// zeroed row kHaloMax.  The host checks the span bound (halo_span_max) before choosing this kernel.
-constexpr int kHaloMax = 184;  // source positions per block (conv2 fwd at 100x13 -> 99x12 needs 182)
-template <int EPI>
-__global__ void __launch_bounds__(kT) conv_halo_split_kernel(NTArgs a) {
-  constexpr int NB = 64, NJ = 2, BM = kBM, CH = 32, LD = CH + 8, Q = CH / 4, NP = 3;
-  constexpr int HPT = ((kHaloMax * Q) + kT - 1) / kT;  // halo float4 per thread
-  constexpr int BPT = NB * Q / kT, RSTEP = kT / Q;
-  __shared__ __attribute__((aligned(16))) __bf16 Hsm[NP][(kHaloMax + 1) * LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][NB * LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * BM;
-  const int HoWo = a.Ho * a.Wo;
-  // span of source rows this block touches (dh in {min_dh, max_dh})
-  int dhmin = a.dh[0], dhmax = a.dh[0];
-#pragma unroll
-  for (int t = 1; t < 4; ++t) {
-    dhmin = min(dhmin, a.dh[t]);
-    dhmax = max(dhmax, a.dh[t]);
-  }
-  const int mlast = min(m0 + BM, a.M) - 1;
-  const int bf = m0 / HoWo, hf = (m0 - bf * HoWo) / a.Wo;
-  const int bl = mlast / HoWo, hl = (mlast - bl * HoWo) / a.Wo;
-  const int64_t s_lo = ((int64_t)bf * a.Hs + max(hf + dhmin, 0)) * a.Ws;
-  const int64_t s_hi = ((int64_t)bl * a.Hs + min(hl + dhmax, a.Hs - 1) + 1) * a.Ws;
-  const int S = (int)(s_hi - s_lo);
-  const __amdgpu_buffer_rsrc_t hrsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.src + s_lo * a.Cs), 0, S * a.Cs * 4, 0x00020000);
-  const int64_t bbytes = (int64_t)a.N * a.ldb * 4;
-  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.Bw), 0, (int)(bbytes < 0x7ffffff0 ? bbytes : 0x7ffffff0), 0x00020000);
-  // this lane's A row (MFMA row lane & 31 of the wave) -> halo position per tap
-  int apos[4];
-  {
-    const int m = m0 + wave * 32 + (lane & 31);
-    const bool rok = m < a.M;
-    const int mm = rok ? m : m0;
-    const int b = mm / HoWo, rem = mm - b * HoWo, h = rem / a.Wo, w = rem - h * a.Wo;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int hs = h + a.dh[t], ws = w + a.dw[t];
-      const bool ok = rok && hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws;
-      apos[t] = ok ? (int)(((int64_t)b * a.Hs + hs) * a.Ws + ws - s_lo) : kHaloMax;
-    }
-  }
-  const int q = tid % Q, r0 = tid / Q;
-  uint32_t boff[BPT];
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    const int n = r0 + RSTEP * j;
-    boff[j] = (uint32_t)(((int64_t)n * a.ldb + 4 * q) * 4);
-  }
-  auto put = [](__bf16* p0, int pstride, float4 v) {
-    f32x2 x[2] = {f32x2{v.x, v.y}, f32x2{v.z, v.w}};
-#pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      uint32_t u[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const bf16x2 r = __builtin_convertvector(x[hh], bf16x2);
-        u[hh] = __builtin_bit_cast(uint32_t, r);
-        if (pl + 1 < NP) {
-          const f32x2 back = {__builtin_bit_cast(float, u[hh] << 16), __builtin_bit_cast(float, u[hh] & 0xffff0000u)};
-          x[hh] -= back;
-        }
-      }
-      *reinterpret_cast<uint2*>(p0 + pl * pstride) = make_uint2(u[0], u[1]);
-    }
-  };
-  // zero row for taps outside the grid
-  if (tid < Q) {
-#pragma unroll
-    for (int pl = 0; pl < NP; ++pl)
-      *reinterpret_cast<uint2*>(&Hsm[pl][kHaloMax * LD + 4 * tid]) = make_uint2(0u, 0u);
-  }
-  f32x16 acc[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-  float4 rb[BPT];
-  auto loadb = [&](int t, int half) {
-    const uint32_t bdelta = (uint32_t)((t * a.Cs + half * CH) * 4);
-#pragma unroll
-    for (int j = 0; j < BPT; ++j)
-      rb[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)(boff[j] + bdelta), 0, 0));
-  };
-  loadb(0, 0);
-  for (int half = 0; half < 2; ++half) {
-    float4 hv[HPT];
-#pragma unroll
-    for (int i = 0; i < HPT; ++i) {
-      const int f = tid + kT * i, pos = f / Q, qq = f % Q;
-      const uint32_t off = pos < S ? (uint32_t)((pos * a.Cs + half * CH + 4 * qq) * 4) : 0x80000000u;
-      hv[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(hrsrc, (int)off, 0, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < HPT; ++i) {
-      const int f = tid + kT * i, pos = f / Q, qq = f % Q;
-      if (pos < kHaloMax) put(&Hsm[0][pos * LD + 4 * qq], (kHaloMax + 1) * LD, hv[i]);
-    }
-    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-      for (int j = 0; j < BPT; ++j) put(&Bs[0][(r0 + RSTEP * j) * LD + 4 * q], NB * LD, rb[j]);
-      __syncthreads();
-      if (t < 3) loadb(t + 1, half);
-      else if (half == 0) loadb(0, 1);
-      const int aoff = apos[t] * LD + 8 * (lane >> 5);
-      const int boff0 = (lane & 31) * LD + 8 * (lane >> 5);
-#pragma unroll
-      for (int ks = 0; ks < CH; ks += 16) {
-        bf16x8 av[NP];
-#pragma unroll
-        for (int pl = 0; pl < NP; ++pl) av[pl] = *reinterpret_cast<const bf16x8*>(&Hsm[pl][aoff + ks]);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          bf16x8 bv[NP];
-#pragma unroll
-          for (int pl = 0; pl < NP; ++pl) bv[pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl][boff0 + j * 32 * LD + ks]);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[j], 0, 0, 0);
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // epilogue: row (r&3) + 8(r>>2) + 4(lane>>5) of the wave's 32, col lane&31 (as gemm_nt_bf16_kernel)
-  float st[NJ][2];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    st[j][0] = st[j][1] = 0.0f;
-    const int col = j * 32 + (lane & 31);
-    float bias = 0.0f;
-    if constexpr (EPI == EPI_CONV) bias = a.bias[col];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m >= a.M) continue;
-      float v = acc[j][r];
-      if constexpr (EPI == EPI_CONV) {
-        v = fmaxf(v + bias, 0.0f);
-        st[j][0] += v;
-        st[j][1] = fmaf(v, v, st[j][1]);
-      }
-      a.out[(int64_t)m * a.ldc + col] = v;
-    }
-  }
-  if constexpr (EPI == EPI_CONV) {
-    if (a.part == nullptr) return;
-    float* red = reinterpret_cast<float*>(&Hsm[0][0]);  // 4 waves x NB x 2 floats, after the last barrier
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
-      const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
-      if (lane < 32) {
-        red[(wave * NB + j * 32 + lane) * 2 + 0] = s0;
-        red[(wave * NB + j * 32 + lane) * 2 + 1] = s1;
-      }
-    }
-    __syncthreads();
-    if (tid < NB) {
-      float s0 = 0.0f, s1 = 0.0f;
-      for (int w = 0; w < 4; ++w) {
-        s0 += red[(w * NB + tid) * 2 + 0];
-        s1 += red[(w * NB + tid) * 2 + 1];
-      }
-      a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
-      a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
-    }
-  }
-}
-
-// TN (weight gradient): slab[blk][n][k] = sum_{m in chunk} D[m][n] * S_t(m)[c], k = t*Cs + c
 struct TNArgs {
   const float* D;
   int ldd;
@@ -2866,88 +2489,6 @@ __device__ __forceinline__ void split3_x8(const float (&x)[8], bf16x8& p0, bf16x
   p2 = __builtin_bit_cast(bf16x8, make_uint4(u[2][0], u[2][1], u[2][2], u[2][3]));
 }
 
-// conv_wgrad_rows_kernel with fp32-accurate products on bf16 MFMA (opt-in: ABD_WGRAD_SPLIT=1 with
-// ABD_PREC_F32_SPLIT; measured 0.21-0.26 ms vs 0.18 ms for the fp32 kernel at B = 512, 100x40 --
-// the strided scalar LDS reads and in-register splits cost more than the MFMA cycles saved): the same
-// row chunks staged by global_load_lds into the same LDS images; the reduction over positions
-// m' runs 16 at a time (v_mfma_f32_32x32x16_bf16: lane half h holds m' = mb + 8h .. +7), each
-// operand split in registers into three exact bf16 planes, six terms per tile.  Positions past
-// the chunk's rows * Ws are masked to zero in the dz operand (their source reads land in the
-// zeroed slack or in finite stale data).
-template <int NB, int CIN>
-__global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds_wg[];
-  constexpr int KT = 4 * CIN / 32, TILES = (NB / 32) * KT, TPW = TILES / 4;
-  static_assert(TILES % 4 == 0 && KT % TPW == 0, "a wave's tiles must share one n-tile");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int half = lane >> 5, col = lane & 31;
-  const int nt = (wave * TPW) / KT;
-  const int rowd = a.Wo * NB / 4;
-  int boff[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int kt = (wave * TPW + i) % KT;
-    const int tap = kt / (CIN / 32), cb = kt % (CIN / 32);
-    boff[i] = ((tap >> 1) * a.Ws + (tap & 1)) * CIN + cb * 32 + col;
-  }
-  for (int i = threadIdx.x; i < 2 * a.bsz; i += kT) lds_wg[i] = 0.0f;
-  __syncthreads();
-  f32x16 acc[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
-  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
-  auto stage = [&](int c, float* buf) {
-    const int b = c / a.cpb, h0 = (c - b * a.cpb) * a.R;
-    const int rows = min(a.R, a.Ho - h0);
-    const float* g = a.dz + ((int64_t)b * a.Ho + h0) * a.Wo * NB;
-    for (int r = 0; r < rows; ++r) glds_copy(g + r * a.Wo * NB, buf + r * a.Ws * NB, rowd);
-    glds_copy(a.src + ((int64_t)b * a.Hs + h0) * a.Ws * CIN, buf + a.dsz, (rows + 1) * a.Ws * CIN / 4);
-  };
-  if (c0 < c1) stage(c0, lds_wg);
-  for (int c = c0; c < c1; ++c) {
-    float* cur = lds_wg + ((c - c0) & 1) * a.bsz;
-    __syncthreads();
-    if (c + 1 < c1) stage(c + 1, lds_wg + ((c + 1 - c0) & 1) * a.bsz);
-    const int h0 = (c % a.cpb) * a.R;
-    const int mlim = min(a.R, a.Ho - h0) * a.Ws;
-    const float* D = cur + nt * 32 + col;
-    const float* S = cur + a.dsz;
-    for (int mb = 0; mb < mlim; mb += 16) {
-      const int m0 = mb + 8 * half;
-      float x[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = (m0 + e < mlim) ? D[(m0 + e) * NB] : 0.0f;
-      bf16x8 a0, a1, a2;
-      split3_x8(x, a0, a1, a2);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = S[(m0 + e) * CIN + boff[i]];
-        bf16x8 b0, b1, b2;
-        split3_x8(x, b0, b1, b2);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[i], 0, 0, 0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[i], 0, 0, 0);
-      }
-    }
-  }
-  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int k = ((wave * TPW + i) % KT) * 32 + col;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      slab[(int64_t)n * (4 * CIN) + k] = acc[i][r];
-    }
-  }
-}
-
 // conv2 weight gradient on bf16 MFMA with fp32-accurate products (ABD_PREC_F32_SPLIT; round 2).
 // dW[n][t*64 + c] = sum_q dz[q][n] * src[q + off(t)][c]: the reduction index q (positions) is the
 // outer NHWC index of both operands, so the MFMA operands are column reads of row-major images.
@@ -2961,151 +2502,8 @@ __global__ void __launch_bounds__(kT, 2) conv_wgrad_rows_split_kernel(WGArgs a) 
 // MFMAs run (registers), then split into the other LDS buffer.  Slabs as conv_wgrad_rows_kernel.
 constexpr int kTrRow = 448;  // bytes per staged position (3 planes x 64 bf16 + pad)
 typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-//   NBUF 1: one image buffer (52 KB for conv2: 3 blocks per CU; chunk c + 1 is written
-//   behind a second barrier once every wave has finished reading chunk c; measured equal, and its 3x
-//   slabs cost more in the reduction); NBUF 2 (default, ABD_WGRAD_TR_BUF): double-buffered
-//   (one barrier per chunk, but 104 KB: one block, i.e. one wave per SIMD)
-template <int R, int NB, int NBUF>  // NB: output channels (64: conv2, 32: conv3); CIN = 64 input channels
-__global__ void __launch_bounds__(kT, NBUF == 1 ? 3 : 2) conv_wgrad_tr_kernel(WGArgs a) {
-  constexpr int CIN = 64, NT = NB / 32, D4 = NB / 4;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_tr[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int Ws = a.Ws, Wo = a.Wo;
-  const int Qd = ((R * Ws + 15) / 16) * 16;  // dz image rows (16-position steps)
-  const int Qs = Qd + Ws + 1;                // source image rows (tap offsets up to Ws + 1)
-  const int nd4 = Qd * D4, ns4 = Qs * 16;    // float4 slots (D4 per dz position, 16 per source position)
-  const int bufb = (Qd + Qs) * kTrRow;
-  const int SLOTS = (nd4 + ns4 + kT - 1) / kT;
-  constexpr int MAXS = 8;  // register staging capacity per thread (checked by the launcher)
-  f32x16 acc[NT][2];
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  const int c0 = blockIdx.x * a.per, c1 = min(a.nchunks, c0 + a.per);
-  float4 st[MAXS];
-  // Slot geometry is fixed across chunks: slot k of this thread reads dz element (row r, column w,
-  // channels 4 c4) or source element (position q, channels 4 c4) of the chunk, at a byte offset
-  // relative to the chunk's first row (off0) plus h0 rows.  Rows past the utterance's last fall
-  // out of the per-utterance buffer descriptor (zeros); the dz pad column and unused slots take
-  // an out-of-range offset.  nd4 is a multiple of 64, so a slot's operand is wave-uniform.
-  constexpr uint32_t kOOB = 0x80000000u;
-  uint32_t off0[MAXS];
-  bool isdz[MAXS];
-#pragma unroll
-  for (int k = 0; k < MAXS; ++k) {
-    const int i = threadIdx.x + k * kT;
-    isdz[k] = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63) + k * kT < nd4;
-    if (i < nd4) {
-      const int q = i / D4, c4 = i % D4, r = q / Ws, w = q - r * Ws;
-      off0[k] = (r < R && w < Wo) ? (uint32_t)(((r * Wo + w) * NB + 4 * c4) * 4) : kOOB;
-    } else {
-      const int q = (i - nd4) >> 4, c4 = (i - nd4) & 15;
-      off0[k] = (k < SLOTS && i < nd4 + ns4 && q < (R + 1) * Ws) ? (uint32_t)((q * CIN + 4 * c4) * 4) : kOOB;
-    }
-  }
-  // global -> registers for chunk c
-  auto fetch = [&](int c) {
-    const int b = c / a.cpb, h0 = (c - b * a.cpb) * R;
-    const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.dz) + (int64_t)b * a.Ho * Wo * NB, 0, a.Ho * Wo * NB * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.src) + (int64_t)b * a.Hs * Ws * CIN, 0, a.Hs * Ws * CIN * 4, 0x00020000);
-    const uint32_t hdz = (uint32_t)(h0 * Wo * NB * 4), hsr = (uint32_t)(h0 * Ws * CIN * 4);
-#pragma unroll
-    for (int k = 0; k < MAXS; ++k) {
-      if (k < SLOTS) {
-        const uint32_t o = off0[k] == kOOB ? kOOB : off0[k] + (isdz[k] ? hdz : hsr);
-        st[k] = __builtin_bit_cast(float4, isdz[k] ? __builtin_amdgcn_raw_buffer_load_b128(rdz, (int)o, 0, 0)
-                                                   : __builtin_amdgcn_raw_buffer_load_b128(rsr, (int)o, 0, 0));
-      }
-    }
-  };
-  // registers -> three exact bf16 planes in image buffer `buf`
-  auto put = [&](unsigned char* buf) {
-#pragma unroll
-    for (int k = 0; k < MAXS; ++k) {
-      const int i = threadIdx.x + k * kT;
-      if (k < SLOTS && i < nd4 + ns4) {
-        const int row = i < nd4 ? i / D4 : Qd + ((i - nd4) >> 4);
-        const int c4 = i < nd4 ? i % D4 : (i - nd4) & 15;
-        f32x2 x[2] = {f32x2{st[k].x, st[k].y}, f32x2{st[k].z, st[k].w}};
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          uint32_t u[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            u[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x[h], bf16x2));
-            if (pl < 2) {
-              const f32x2 back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
-              x[h] -= back;
-            }
-          }
-          *reinterpret_cast<uint2*>(buf + row * kTrRow + pl * 128 + c4 * 8) = make_uint2(u[0], u[1]);
-        }
-      }
-    }
-  };
-  // transposed fragment of image rows [row0 + 8h, +8) at columns 32 tile + (lane & 31), plane pl
-  const int g = (lane >> 4) & 1, h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
-  auto frag = [&](const unsigned char* img, int row0, int tile, int pl) -> bf16x8 {
-    const int col = 32 * tile + 16 * g + 4 * pp;
-    const unsigned char* p = img + (row0 + 8 * h + qq) * kTrRow + pl * 128 + col * 2;
-    const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p));
-    const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4v*)(p + 4 * kTrRow));
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  const int toff = (wave >> 1) * Ws + (wave & 1);  // this wave's tap (dh, dw) as a position offset
-  if (c0 < c1) {
-    fetch(c0);
-    put(lds_tr);
-  }
-  for (int c = c0; c < c1; ++c) {
-    __syncthreads();  // chunk c's images are complete; the other buffer is free
-    const unsigned char* cur = lds_tr + (NBUF == 2 ? ((c - c0) & 1) * bufb : 0);
-    if (c + 1 < c1) fetch(c + 1);  // in flight while the MFMAs run
-    const unsigned char* dzi = cur;
-    const unsigned char* sri = cur + Qd * kTrRow;
-    for (int q0 = 0; q0 < Qd; q0 += 16) {
-      bf16x8 av[NT][3], bv[2][3];
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) av[t][pl] = frag(dzi, q0, t, pl);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) bv[t][pl] = frag(sri, q0 + toff, t, pl);
-      }
-      constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};  // a2b0 a0b2 a1b1 a1b0 a0b1 a0b0
-#pragma unroll
-      for (int term = 0; term < 6; ++term)
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][TA[term]], bv[j][TB[term]], acc[i][j], 0, 0, 0);
-    }
-    if (c + 1 < c1) {
-      if constexpr (NBUF == 1) __syncthreads();  // every wave is done with chunk c's images
-      put(lds_tr + (NBUF == 2 ? ((c + 1 - c0) & 1) * bufb : 0));
-    }
-  }
-  // slab: D[n][c] of tap `wave`: row n = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col c = 32 j + (lane & 31)
-  float* slab = a.slab + (int64_t)blockIdx.x * NB * (4 * CIN);
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int n = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        slab[(int64_t)n * (4 * CIN) + wave * CIN + 32 * j + (lane & 31)] = acc[i][j][r];
-      }
-}
-
-// Software-pipelined variant of conv_wgrad_tr_kernel (default; ABD_WGRAD_TRP=0 restores the
-// kernel above).  One 4-wave block per CU (the double-buffered images take 104 KB), so a wave has
+// Software-pipelined transpose-read weight gradient (the round-2 kernel, conv_wgrad_tr_kernel, had
+// the same staging without the pipeline; it is gone).  One 4-wave block per CU (the double-buffered images take 104 KB), so a wave has
 // no partner on its SIMD to hide its non-MFMA work: every chunk's staging is moved inside the
 // previous chunk's MFMA stream instead.
 //   * chunk c + 2's global loads are issued at the top of chunk c (two chunks ahead: a whole
@@ -3115,8 +2513,7 @@ __global__ void __launch_bounds__(kT, NBUF == 1 ? 3 : 2) conv_wgrad_tr_kernel(WG
 //   * the next 16-position step's fragments are read after the current step's first term, so the
 //     LDS latency is off the MFMA path and the lgkmcnt range (15) still covers the older reads.
 // NS = Qd / 16 steps and MAXS staging slots are compile-time (checked by the launcher); slots
-// past the images write a trash row (row Qd + Qs of each buffer).  Same sums as the kernel above
-// in the same order: the results are bit-identical.
+// past the images write a trash row (row Qd + Qs of each buffer).
 #ifndef ABD_TRP_ABL  // ablation bits (measurement builds): 1 no MFMAs, 2 no staging writes, 4 no loads
 #define ABD_TRP_ABL 0
 #endif
@@ -3614,15 +3011,6 @@ struct abd_cnn {
   int max_batch;
   int64_t off[P_COUNT + 1];
   int precision = ABD_PREC_F32_SPLIT;  // abd_smallcnn_set_precision (include/abd.h)
-  // weight-gradient side stream (created on first use): conv3 / conv2 weight gradients run there,
-  // concurrently with the data-gradient chain of the caller's stream, joined before return
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  ~abd_cnn() {
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (side) (void)hipStreamDestroy(side);
-  }
 };
 
 namespace {
@@ -3659,9 +3047,9 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
-int c1_rows() { return std::max(1, std::min(kR1, env_int("ABD_C1_ROWS", 8))); }
+int c1_rows() { return kR1; }
 int64_t nchunks_conv1(const Geo& g, int64_t B) { return B * ((g.H1 + c1_rows() - 1) / c1_rows()); }
-int64_t nblk_conv1(const Geo& g, int64_t B) { return std::min<int64_t>(nchunks_conv1(g, B), env_int("ABD_C1_CAP", 2048)); }
+int64_t nblk_conv1(const Geo& g, int64_t B) { return std::min<int64_t>(nchunks_conv1(g, B), 2048); }
 // resident blocks of conv1_stats_fold_kernel over the device
 int64_t c1f_blocks() {
   static int64_t n = 0;
@@ -3685,7 +3073,7 @@ int64_t c1w_blocks() {
     (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&conv1_wgrad_kernel<FULL>),
                                                        kT, 0);
-    n = env_int("ABD_C1W_CAP", 0) > 0 ? env_int("ABD_C1W_CAP", 0) : (int64_t)cu * std::max(1, per);
+    n = (int64_t)cu * std::max(1, per);
   }
   return n;
 }
@@ -3700,20 +3088,16 @@ HeadPlan head_plan(const Geo& g, int64_t B) {
   HeadPlan h;
   h.rt = (int)((B + 31) / 32);
   const int P = g.flat / 32;
-  static const int force = env_int("ABD_HEAD_PP", 0);
   h.pp = 1;
   while (h.pp < 8 && (int64_t)h.rt * ((P + h.pp - 1) / h.pp) > 512) h.pp *= 2;
-  if (force == 1 || force == 2 || force == 4 || force == 8) h.pp = force;
   h.ks = (P + h.pp - 1) / h.pp;
   h.nft = g.flat / 32;
   h.nrb = (int)((B + kHeadRB - 1) / kHeadRB);
   return h;
 }
-// the train step runs the fused fc head (ABD_FC_HEAD=0 restores the round-2 launches)
-bool head_on() {
-  static const bool on = env_int("ABD_FC_HEAD", 1) != 0;
-  return on;
-}
+// the single-rank train step runs the fused fc head; SyncBN steps keep the round-2 launches (BN3's
+// sums are all-reduced between the loss and the BN3 backward)
+bool head_on() { return true; }
 
 PoolArgs pool_args(const Geo& g, int layer, int64_t B);
 int head_napply(const PoolArgs& a, int64_t B);
@@ -3893,10 +3277,6 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.n_w1 = 4 * ((g.flat + 31) / 32);
   a.n_w2 = 4 * ((g.K + 31) / 32) + (g.K + 128 + kHeadW2 - 1) / kHeadW2;  // fc2 weight tiles + bias sums
   a.n_apply = head_napply(a.pool, B);
-  // timing ablations (results invalid): bit 0 drops the fc1 weight-gradient tiles, bit 1 the BN3 apply
-  static const int abl = env_int("ABD_HEAD_ABL", 0);
-  if (abl & 1) a.n_w1 = 0;
-  if (abl & 2) a.n_apply = 0;
   return a;
 }
 
@@ -3988,51 +3368,6 @@ TNArgs conv_wgrad_args(const float* dz, int Cout, const float* src, int Hs, int 
   return a;
 }
 
-// Row-chunk wgrad launch (conv_wgrad_rows_kernel); returns the slab count, -1 on error.
-// R = output rows per chunk (ABD_WGRAD_R<layer> overrides, for tuning); the grid is the
-// resident block count (occupancy API) capped by the slab buffer.
-// conv_wgrad_tr_kernel<R, NB> launch (64 input channels); -1 when the geometry does not fit
-template <int R, int NB, int NBUF>
-int launch_wgrad_tr_n(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
-                    float* slab, int phase, hipStream_t s) {
-  if (Ws != Wo + 1 || Hs < Ho + 1) return -1;
-  WGArgs a{};
-  a.dz = dz;
-  a.src = src;
-  a.Ho = Ho;
-  a.Wo = Wo;
-  a.Hs = Hs;
-  a.Ws = Ws;
-  a.R = R;
-  a.cpb = (Ho + R - 1) / R;
-  a.nchunks = (int)(B * a.cpb);
-  a.slab = slab;
-  const int Qd = ((R * Ws + 15) / 16) * 16, Qs = Qd + Ws + 1;
-  if (Qd * (NB / 4) + Qs * 16 > 8 * kT) return -1;  // register staging capacity (MAXS)
-  const size_t lds = NBUF * (size_t)(Qd + Qs) * kTrRow;
-  static size_t cached = 0;
-  static int per_cu = 1, n_cu = 256;
-  if (cached != lds) {
-    ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB, NBUF>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int dev = 0;
-    ABD_HIP(hipGetDevice(&dev));
-    ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv_wgrad_tr_kernel<R, NB, NBUF>),
-                                                         kT, lds));
-    per_cu = std::max(1, per_cu);
-    cached = lds;
-  }
-  int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
-  a.per = (a.nchunks + grid - 1) / grid;
-  grid = (a.nchunks + a.per - 1) / a.per;
-  if (phase >= 0) abd::prof_begin(phase, s);
-  conv_wgrad_tr_kernel<R, NB, NBUF><<<grid, kT, lds, s>>>(a);
-  if (phase >= 0) abd::prof_end(phase, s);
-  ABD_LAUNCH_CHECK();
-  return grid;
-}
-
 // conv_wgrad_trp_kernel<R, NB, NS, MAXS> launch; -1 when the geometry is not this instantiation's
 // geometry check of conv_wgrad_trp_kernel<R, NB, NS, MAXS, ...> (also used to decide the plane mode)
 template <int R, int NB, int NS, int MAXS>
@@ -4111,34 +3446,29 @@ int launch_wgrad_tr_planes(int Ho, int Wo, int Hs, int Ws, int64_t B, int max_sl
   if (r < 0) r = launch_wgrad_trp_n<R, 64, 1, 4, NP, true>(nullptr, nullptr, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s, &pl);
   return r;
 }
+// the transpose-read weight gradient for the f32split / bf16 modes: the first trp instantiation
+// whose staging fits the geometry (conv2 at W = 40, Ws = 13: 6-row chunks fill 72 of 80 staged
+// positions; 2-row: 24 of 32), -1 when none does (the caller then takes conv_wgrad_rows_kernel)
 template <int R, int NB, int NP = 3>
 int launch_wgrad_tr(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int max_slabs,
                     float* slab, int phase, hipStream_t s) {
-  static const bool trp = env_int("ABD_WGRAD_TRP", 1) != 0;
-  if (trp || NP == 1) {
-    int r = -1;
-    // conv2 at W = 40 (Ws = 13): 6-row chunks fill 72 of 80 staged positions (2-row: 24 of 32)
-    static const int r6 = env_int("ABD_WGRAD_TRP_R6", 1);
-    if constexpr (NB == 64) {
-      if (r6) r = launch_wgrad_trp_n<6, NB, 5, 11, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 2, 5, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 8, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-    } else {
-      r = launch_wgrad_trp_n<R, NB, 2, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 6, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-      if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 2, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
-    }
-    if (r >= 0 || NP == 1) return r;
+  int r = -1;
+  if constexpr (NB == 64) {
+    r = launch_wgrad_trp_n<6, NB, 5, 11, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    if (r < 0) r = launch_wgrad_trp_n<R, NB, 2, 5, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 8, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+  } else {
+    r = launch_wgrad_trp_n<R, NB, 2, 4, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    if (r < 0) r = launch_wgrad_trp_n<R, NB, 3, 6, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+    if (r < 0) r = launch_wgrad_trp_n<R, NB, 1, 2, NP>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
   }
-  static const int nbuf = env_int("ABD_WGRAD_TR_BUF", 2);
-  return nbuf == 2 ? launch_wgrad_tr_n<R, NB, 2>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s)
-                   : launch_wgrad_tr_n<R, NB, 1>(dz, src, Ho, Wo, Hs, Ws, B, max_slabs, slab, phase, s);
+  return r;
 }
 
 template <int NB, int CIN>
 int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs, int Ws, int64_t B, int R,
-                      int max_slabs, float* slab, int phase, hipStream_t s, bool split = false) {
+                      int max_slabs, float* slab, int phase, hipStream_t s) {
   ABD_CHECK(Ws == Wo + 1 && Hs >= Ho + 1, ABD_E_UNSUPPORTED, "wgrad geometry");
   WGArgs a{};
   a.dz = dz;
@@ -4152,17 +3482,14 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
   a.nchunks = (int)(B * a.cpb);
   // dz on the Ws-strided grid; source rows + one slack row (a pad position's dh = 1 tap
   // reads one row past the chunk)
-  // split: 16-position groups read up to 15 positions past the chunk (masked dz; source slack)
-  const int slackp = split ? 16 : 2;
-  a.dsz = ((a.R * Ws + slackp) * NB + 3) & ~3;  // + positions for the one-ahead / group read
-  a.bsz = (a.dsz + ((a.R + 2) * Ws + (split ? 16 : 0)) * CIN + 3) & ~3;
+  a.dsz = ((a.R * Ws + 2) * NB + 3) & ~3;  // + positions for the one-ahead read
+  a.bsz = (a.dsz + (a.R + 2) * Ws * CIN + 3) & ~3;
   a.slab = slab;
   const size_t lds = 2 * (size_t)a.bsz * sizeof(float);
-  auto* kern = split ? &conv_wgrad_rows_split_kernel<NB, CIN> : &conv_wgrad_rows_kernel<NB, CIN>;
-  static size_t cached_lds[2] = {0, 0};
-  static int per_cu_c[2] = {1, 1}, n_cu = 256;
-  int& per_cu = per_cu_c[split];
-  if (cached_lds[split] != lds) {
+  auto* kern = &conv_wgrad_rows_kernel<NB, CIN>;
+  static size_t cached_lds = 0;
+  static int per_cu = 1, n_cu = 256;
+  if (cached_lds != lds) {
     ABD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
     int dev = 0;
@@ -4170,7 +3497,7 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
     ABD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     ABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kT, lds));
     per_cu = std::max(1, per_cu);
-    cached_lds[split] = lds;
+    cached_lds = lds;
   }
   int grid = (int)std::min<int64_t>({(int64_t)a.nchunks, (int64_t)n_cu * per_cu, (int64_t)max_slabs});
   a.per = (a.nchunks + grid - 1) / grid;
@@ -4183,38 +3510,7 @@ int launch_wgrad_rows(const float* dz, const float* src, int Ho, int Wo, int Hs,
 }
 
 
-// conv_halo_split_kernel when the geometry fits it (2x2 taps, 64 -> 64 channels, every block's
-// source span <= kHaloMax positions, checked exactly here), else -1: the caller then runs the
-// im2col split GEMM.  Opt-in (ABD_HALO=1): measured 0.1845 vs 0.177 ms (conv2 fwd, B = 512) --
-// the im2col kernel is issue/barrier-bound, not load- or conversion-bound.
-template <int EPI>
-int launch_conv_halo_split(const NTArgs& a, hipStream_t s, int phase) {
-  static const bool on = env_int("ABD_HALO", 0) != 0;  // measured slower: opt-in
-  if (!on || a.Cs != 64 || a.N != 64 || a.taps != 4 || a.ksplit > 1 || a.ldb != 256) return -1;
-  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != (a.M + kBM - 1) / kBM) return -1;
-  int dhmin = a.dh[0], dhmax = a.dh[0];
-  for (int t = 1; t < 4; ++t) {
-    dhmin = std::min(dhmin, a.dh[t]);
-    dhmax = std::max(dhmax, a.dh[t]);
-    if (a.dw[t] < -1 || a.dw[t] > 1) return -1;
-  }
-  const int HoWo = a.Ho * a.Wo;
-  for (int64_t m0 = 0; m0 < a.M; m0 += kBM) {
-    const int64_t ml = std::min<int64_t>(m0 + kBM, a.M) - 1;
-    const int64_t bf = m0 / HoWo, hf = (m0 - bf * HoWo) / a.Wo, bl = ml / HoWo, hl = (ml - bl * HoWo) / a.Wo;
-    const int64_t lo = (bf * a.Hs + std::max<int64_t>(hf + dhmin, 0)) * a.Ws;
-    const int64_t hi = (bl * a.Hs + std::min<int64_t>(hl + dhmax, a.Hs - 1) + 1) * a.Ws;
-    if (hi - lo > kHaloMax) return -1;
-  }
-  dim3 grid((a.M + kBM - 1) / kBM, 1, 1);
-  if (phase >= 0) abd::prof_begin(phase, s);
-  conv_halo_split_kernel<EPI><<<grid, dim3(kT), 0, s>>>(a);
-  if (phase >= 0) abd::prof_end(phase, s);
-  ABD_LAUNCH_CHECK();
-  return 0;
-}
-
-// conv_ws_split_kernel: persistent blocks, one per CU (ABD_WS=0 restores gemm_nt_bf16_kernel)
+// conv_ws_split_kernel / conv_ws_dma_kernel: persistent blocks, one per CU
 int ws_grid() {
   static int n = 0;
   if (n == 0) {
@@ -4225,24 +3521,24 @@ int ws_grid() {
   }
   return n;
 }
-bool ws_on() {
-  static const bool on = env_int("ABD_WS", 1) != 0;
-  return on;
-}
-// blocks of a launch: one 8-wave block per CU.  conv3 (48 KB of weights, 132-190 VGPRs) also fits
-// only one 8-wave block per CU, so ABD_WS3_MULT=2 runs its second block per CU as a second round
-// (measured: conv3 fwd 0.037 -> 0.033 ms, dgrad 0.031 -> 0.026 ms with one)
-// Small problems (FlowMur's 32 x 13 input: conv2 has 23 k rows at B = 256) get no more blocks than
-// give every wave one 32-row tile: each block stages the whole weight operand into its LDS, so the
-// full grid would stage it 256 times for ~11 rows per wave (ABD_WS_MIN_TILES: tiles per wave)
+// blocks of a launch: one 8-wave block per CU (conv3's 48 KB of weights and 132-190 VGPRs also fit
+// only one).  Small problems (FlowMur's 32 x 13 input: conv2 has 23 k rows at B = 256) get no more
+// blocks than give every wave one 32-row tile: each block stages the whole weight operand into its
+// LDS, so the full grid would stage it 256 times for ~11 rows per wave.
 int ws_blocks(int N, int Cs, int64_t M) {
-  static const int m3 = std::max(1, env_int("ABD_WS3_MULT", 1));
-  static const int mt = std::max(0, env_int("ABD_WS_MIN_TILES", 1));
-  const int full = (N == 64 && Cs == 64) ? ws_grid() : m3 * ws_grid();
-  if (mt == 0) return full;
-  const int64_t need = (M + 8 * 32 * (int64_t)mt - 1) / (8 * 32 * (int64_t)mt);  // 8-wave blocks
-  return (int)std::max<int64_t>(1, std::min<int64_t>(full, need));
+  (void)N;
+  (void)Cs;
+  const int64_t need = (M + 8 * 32 - 1) / (8 * 32);  // 8-wave blocks
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ws_grid(), need));
 }
+// 32-bit buffer offsets of the weight-stationary kernels (their A operand is one buffer resource)
+bool ws_fits(const NTArgs& a) {
+  return a.taps == 4 && a.ksplit <= 1 && a.ldb == 4 * a.Cs && a.ldc == a.N &&
+         (int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) < 0x7ffffff0LL;
+}
+// ABD_WS_DMA: 0 direct-load kernel everywhere, 1 (default) LDS-DMA kernel for the forward GEMMs,
+// 2 LDS-DMA for the data gradients too (read at each launch: tests/test_gpu_conv_tiles.py runs all three)
+int ws_dma_mode() { return env_int("ABD_WS_DMA", 1); }
 // Largest staged span (positions) of any 32 consecutive output rows of conv_ws_dma_kernel: the
 // rows' source indices repeat with the image (period Ho*Wo), so every window over two images plus
 // one tile is scanned once per geometry (cached).
@@ -4277,43 +3573,36 @@ int dma_span(const NTArgs& a) {
 }
 template <int EPI, int NP = 3, bool PA = false>
 int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
-  if (!ws_on() || a.taps != 4 || a.ksplit > 1 || a.ldb != 4 * a.Cs || a.ldc != a.N) return -1;
+  if (!ws_fits(a)) return -1;
   if (PA && (a.srcs == nullptr || a.N != 64 || a.Cs != 64)) return -1;
   const int nb = ws_blocks(a.N, a.Cs, a.M);
   if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
-  if ((int64_t)a.Hs * a.Ws * a.Cs * 4 * (a.M / (a.Ho * a.Wo)) >= 0x7ffffff0LL) return -1;  // 32-bit buffer offsets
   if (phase >= 0) abd::prof_begin(phase, s);
-  static const int cfg = env_int("ABD_WS_CFG", 2);  // conv2 tile / ring / waves-per-block (A/B knob)
   // K-step order (see the kernel): channel-group-major for the forward (conv2 0.147 -> 0.141 ms),
-  // tap-major for the data gradient (0.133 vs 0.136 ms channel-major); ABD_WS_KORD 0 / 1 / 2 =
-  // tap-major everywhere / forward only / both
-  static const int kord = env_int("ABD_WS_KORD", 1);
-  const bool ko = kord == 2 || (kord == 1 && EPI == EPI_CONV);
+  // tap-major for the data gradient (0.133 vs 0.136 ms channel-major)
+  const bool ko = EPI == EPI_CONV;
   // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the data gradient
   // measured slower through it (0.132 -> 0.141 ms: its tap masks and edge rows), so it stays on the
-  // direct kernel.  ABD_WS_DMA = 0 / 1 / 2: direct everywhere / DMA forward (default) / DMA both
-  static const int dma_mode = env_int("ABD_WS_DMA", 1);
+  // direct kernel by default (ws_dma_mode)
+  const int dma_mode = ws_dma_mode();
   const bool dma = dma_mode == 2 || (dma_mode == 1 && EPI == EPI_CONV);
   // the forward's taps never leave the source grid; the data gradient's are masked in the kernel
   const bool fwd_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == 1 && a.dh[2] == 1 && a.dw[2] == 0 &&
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
   const bool dg_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == -1 && a.dh[2] == -1 && a.dw[2] == 0 &&
                        a.dh[3] == -1 && a.dw[3] == -1;
-  // conv3 (N = 32) through the same kernel with one 32-column tile per wave (ABD_WS_DMA3=0: direct)
-  static const bool dma3 = env_int("ABD_WS_DMA3", 1) != 0;
-  if (!PA && dma && (a.N == 64 || (a.N == 32 && dma3)) && a.Cs == 64 &&
+  // conv3 (N = 32) through the same kernel with one 32-column tile per wave
+  if (!PA && dma && (a.N == 64 || a.N == 32) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
     if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_dma_kernel<EPI, NP, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true><<<dim3(nb), dim3(512), 0, s>>>(a);
-  } else if (NP == 3 && a.N == 64 && a.Cs == 64 && cfg == 1) conv_ws_split_kernel<EPI, 2, 64, 1, 4, 16, NP><<<dim3(nb), dim3(1024), 0, s>>>(a);
-  else if (a.N == 64 && a.Cs == 64 && (cfg == 2 || NP == 1)) {
+  } else if (a.N == 64 && a.Cs == 64) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, false, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  } else if (NP == 3 && a.N == 64 && a.Cs == 64) conv_ws_split_kernel<EPI, 2, 64, 2, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
-  else if (a.N == 32 && a.Cs == 64) {
+  } else if (a.N == 32 && a.Cs == 64) {
     if (ko) conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP, false, true><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_split_kernel<EPI, 1, 64, 1, 4, 8, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (a.N == 64 && a.Cs == 32) {
@@ -4328,54 +3617,10 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   return 0;
 }
 
-// K-chunk depth of the 3-plane conv2 GEMMs (ABD_SPLIT_KB=16: 28 KB of LDS per block, 4 waves/SIMD)
-static int split_kb() {
-  static const int kb = env_int("ABD_SPLIT_KB", 32) == 16 ? 16 : 32;
-  return kb;
-}
-
-// rows per wave (x32) of the 3-plane conv2 GEMMs; ABD_SPLIT_MI=1 restores the 128-row tiles
-static int split_mi() {
-  static const int mi = env_int("ABD_SPLIT_MI", 1) == 1 ? 1 : 2;
-  return mi;
-}
-
-// prefetch distance of the 3-plane GEMMs (ABD_SPLIT_PD=1: loads one chunk ahead)
-static int split_pd() {
-  static const int pd = env_int("ABD_SPLIT_PD", 2) == 1 ? 1 : 2;
-  return pd;
-}
-
-template <int NB, int EPI, int KB, int NP = 1, int MI = 1>
-int launch_nt_bf16(const NTArgs& a, hipStream_t s, int phase) {
-  if (a.Cs % KB != 0 || a.ksplit > 1) return -1;
-  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != (a.M + kBM * MI - 1) / (kBM * MI)) return -1;
-  dim3 grid((a.M + kBM * MI - 1) / (kBM * MI), (a.N + NB - 1) / NB, 1);
-  if (phase >= 0) abd::prof_begin(phase, s);
-  if (NP == 3 && split_pd() == 2) gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI, 2><<<grid, dim3(kT), 0, s>>>(a);
-  else gemm_nt_bf16_kernel<NB, EPI, KB, NP, MI, 1><<<grid, dim3(kT), 0, s>>>(a);
-  if (phase >= 0) abd::prof_end(phase, s);
-  ABD_LAUNCH_CHECK();
-  return 0;
-}
-
-// grid.x of an NT launch: one block per 128*MI-row tile, or (ABD_NT_PERSIST = k > 0) at most
-// k blocks per CU x resident blocks, each looping over tiles -- EPI_CONV's a.nblk must match.
+// grid.x of an NT launch: one block per 128*MI-row tile (EPI_CONV's a.nblk must match)
 template <int NB, int EPI, int MI = 1>
 int nt_grid_x(const NTArgs& a) {
-  const int mtiles = (a.M + kBM * MI - 1) / (kBM * MI);
-  static const int persist = env_int("ABD_NT_PERSIST", 0);
-  if (persist <= 0 || a.ksplit > 1) return mtiles;
-  static int cap = 0;
-  if (cap == 0) {
-    int dev = 0, n_cu = 256, per_cu = 1;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(gemm_nt_kernel<NB, EPI, MI>),
-                                                       kT, 0);
-    cap = std::max(1, n_cu * std::max(1, per_cu) * persist / 4);
-  }
-  return std::min(mtiles, cap);
+  return (a.M + kBM * MI - 1) / (kBM * MI);
 }
 
 template <int NB, int EPI, int MI = 1, int KC = kKC>
@@ -4480,21 +3725,6 @@ int bn_bwd_finalize(const BnSync& y, int point, const float* part, int nblk, int
   return 0;
 }
 
-// backward coefficients of the BatchNorm feeding a 2x2 conv, from the conv's gradients
-// (bn_bwd_derived_kernel); W, G: (Cout, Cin, 2, 2), db: (Cout)
-int bn_bwd_derive(const BnSync& y, int point, const float* W, const float* G, const float* db, int Cout, int Cin,
-                  double count, const float* gamma, const float* beta, const float4* coef, float* dgamma, float* dbeta,
-                  BCoef* bcoef, hipStream_t s) {
-  double* buf = y.on() ? y.buf + (int64_t)point * ABD_BN_SYNC_STRIDE : nullptr;
-  bn_bwd_derived_kernel<<<Cin, kT, 0, s>>>(W, G, db, Cout, Cin, gamma, beta, coef, count, dgamma, dbeta, bcoef, buf);
-  ABD_LAUNCH_CHECK();
-  if (!y.on()) return 0;
-  if (sync_point(y, point, Cin)) return -1;
-  bn_sync_bwd_finalize_kernel<<<1, 64, 0, s>>>(buf, Cin, gamma, coef, bcoef);
-  ABD_LAUNCH_CHECK();
-  return 0;
-}
-
 // -------------------------------------------------------------- forward (train or eval)
 int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_t B, const float* running_in,
             float* running_upd, bool train, const DropArgs& drop1, const DropArgs& drop2, hipStream_t s,
@@ -4572,13 +3802,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   // ---- layer 2: conv2 (MFMA) + relu + stats -> BN2 -> pool2
   {
     NTArgs a = conv_fwd_args(w.p1, g.H1, g.W1p, 64, g.H2, g.W2, B, w.w2f, 64, P.p[P_C2B], w.r2);
-    static const bool mi2 = env_int("ABD_NT_MI2", 0) != 0;
     const bool bf = net->precision == ABD_PREC_BF16, sp = net->precision == ABD_PREC_F32_SPLIT;
-    const bool ws = (sp || bf) && ws_on();  // bf16: the same weight-stationary kernel on one plane
-    a.nblk = ws ? ws_blocks(64, 64, a.M)
-             : bf ? (a.M + kBM - 1) / kBM
-             : sp ? (a.M + kBM * split_mi() - 1) / (kBM * split_mi())
-             : mi2 ? nt_grid_x<64, EPI_CONV, 2>(a) : nt_grid_x<64, EPI_CONV>(a);
+    // f32split / bf16: the weight-stationary kernels (bf16 on one plane); fp32 MFMA otherwise, and
+    // for a batch past their 32-bit buffer offsets
+    const bool ws = (sp || bf) && ws_fits(a);
+    a.nblk = ws ? ws_blocks(64, 64, a.M) : nt_grid_x<64, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     // p1 holds m under the BN1 fold: only the weight-stationary split kernel applies it (bn1_fold_ok)
     ABD_CHECK(!fold1 || ws, ABD_E_UNSUPPORTED, "BN1 fold needs the weight-stationary conv2 kernel");
@@ -4586,23 +3814,14 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
       a.Bw = w.w2fold;
       a.fold_t = w.ft2;
     }
-    static const bool kc64 = env_int("ABD_NT_KC64", 0) != 0;
     if (planes > 0) {
       a.srcs = w.p1s;
       a.splane = B * g.H1 * g.W1p * 64;
     }
-    if (planes == 3 ? launch_conv_ws_split<EPI_CONV, 3, true>(a, s, abd::PH_CONV2_FWD)
-        : planes == 1 ? launch_conv_ws_split<EPI_CONV, 1, true>(a, s, abd::PH_CONV2_FWD)
+    if (planes == 1 ? launch_conv_ws_split<EPI_CONV, 1, true>(a, s, abd::PH_CONV2_FWD)
         : ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
-                 : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD))
-           : bf ? launch_nt_bf16<64, EPI_CONV, 64>(a, s, abd::PH_CONV2_FWD)
-           : sp ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_CONV, 32, 3, 2>(a, s, abd::PH_CONV2_FWD)
-                   : launch_conv_halo_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD) == 0
-                       ? 0
-                   : split_kb() == 16 ? launch_nt_bf16<64, EPI_CONV, 16, 3>(a, s, abd::PH_CONV2_FWD)
-                                      : launch_nt_bf16<64, EPI_CONV, 32, 3>(a, s, abd::PH_CONV2_FWD))
-           : mi2 ? launch_nt<64, EPI_CONV, 2>(a, s, abd::PH_CONV2_FWD)
-           : kc64 ? launch_nt<64, EPI_CONV, 1, 64>(a, s, abd::PH_CONV2_FWD) : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+                   : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD))
+             : launch_nt<64, EPI_CONV>(a, s, abd::PH_CONV2_FWD))
       return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
@@ -4628,14 +3847,12 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
   {
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
-    const bool ws3 = (sp3 || bf3) && ws_on();
-    a.nblk = ws3 ? ws_blocks(32, 64, a.M) : (bf3 || sp3) ? (a.M + kBM - 1) / kBM : nt_grid_x<32, EPI_CONV>(a);
+    const bool ws3 = (sp3 || bf3) && ws_fits(a);
+    a.nblk = ws3 ? ws_blocks(32, 64, a.M) : nt_grid_x<32, EPI_CONV>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    if (ws3   ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
-                     : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))
-        : bf3 ? launch_nt_bf16<32, EPI_CONV, 64>(a, s, abd::PH_CONV3_FWD)
-        : sp3 ? launch_nt_bf16<32, EPI_CONV, 32, 3>(a, s, abd::PH_CONV3_FWD)
-              : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
+    if (ws3 ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
+                   : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))
+            : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
       return -1;
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
@@ -4711,20 +3928,11 @@ int loss_and_metrics(abd_cnn* net, const Work& w, const Params& P, const int64_t
   return 0;
 }
 
-// BN2 / BN1 backward statistics derived from the next conv's weight / bias gradients
-// (bn_bwd_derived_kernel); ABD_BN_BWD_STATS=0 restores the passes over the activations
-// (bn_pool_bwd_stats_kernel / conv1_bwd_stats_kernel).
-bool bn_bwd_derived_on() {
-  static const bool on = env_int("ABD_BN_BWD_STATS", 1) != 0;
-  return on;
-}
-
-// The train step folds BN1 into conv2 (conv1_stats_fold_kernel; ABD_BN1_FOLD=0 restores the separate
-// conv1_bn_pool pass) when conv2's forward runs on the weight-stationary split kernel.
+// The train step folds BN1 into conv2 (conv1_stats_fold_kernel; the separate conv1_bn_pool pass
+// remains for f32, SyncBN and per-utterance steps) when conv2's forward runs on the
+// weight-stationary split kernel (ws_fits: 32-bit buffer offsets).
 bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
-  static const bool on = env_int("ABD_BN1_FOLD", 1) != 0;
-  return on && (net->precision == ABD_PREC_F32_SPLIT || net->precision == ABD_PREC_BF16) && ws_on() &&
-         split_mi() == 1 &&
+  return (net->precision == ABD_PREC_F32_SPLIT || net->precision == ABD_PREC_BF16) &&
          (int64_t)g.H1 * g.W1p * 64 * 4 * B < 0x7ffffff0LL;
 }
 // conv2 plane mode: the train step keeps conv2's two activation operands -- the pool1 output m (BN1
@@ -4734,52 +3942,17 @@ bool bn1_fold_ok(const abd_cnn* net, const Geo& g, int64_t B) {
 // f32split, 1 in bf16) or 0 (fp32 buffers).  Measured (r3_v2, B = 512 ultrasonic): in f32split the
 // planes are 6 B per element against fp32's 4, and the weight-stationary GEMMs re-read every operand
 // row for 4 taps from L2 -- conv2 forward 0.144 -> 0.235 ms, data gradient 0.129 -> 0.184, weight
-// gradient 0.121 -> 0.152, BN2 backward +11 us: off by default there (ABD_PLANES=3 enables it).
-// bf16 (one 2-B plane) halves the operand bytes instead: on by default (ABD_PLANES=0 disables).
+// gradient 0.121 -> 0.152, BN2 backward +11 us: bf16 only (one 2-B plane halves the operand bytes).
 int conv2_planes(const abd_cnn* net, const Geo& g, int64_t B, bool fold1) {
-  static const int mode = env_int("ABD_PLANES", 1);  // 0 off, 1 bf16 only, 3 bf16 and f32split
-  if (mode == 0 || !fold1) return 0;
-  const int np = (net->precision == ABD_PREC_F32_SPLIT && mode == 3) ? 3 : net->precision == ABD_PREC_BF16 ? 1 : 0;
-  if (np == 0 || !ws_on() || split_mi() != 1 || (np == 3 && env_int("ABD_WS_CFG", 2) != 2)) return 0;
+  if (!fold1) return 0;
+  const int np = net->precision == ABD_PREC_BF16 ? 1 : 0;
+  if (np == 0) return 0;
   const int64_t n_p1 = B * g.H1 * g.W1p * 64, n_r2 = B * g.H2 * g.W2 * 64;
   if ((int64_t)3 * std::max(n_p1, n_r2) * 2 >= 0x7ffffff0LL) return 0;  // 32-bit buffer offsets
   if (!trp_planes_fit<2>(g.H2, g.W2, g.H1, g.W1p)) return 0;
   return np;
 }
 
-// Stream for the conv weight gradients: they depend only on dz and the stored forward activations and
-// feed nothing but the final gradient buffer, so they run on a side stream of the net while the data-
-// gradient chain (dgrad -> BN backward -> ...) continues on the caller's stream; backward() joins it
-// before returning.  Opt-in (ABD_WGRAD_SIDE=1): measured 2-4 % slower per step than one stream
-// (the weight-gradient and data-gradient kernels compete for the same CUs; with the derived BN
-// statistics the chain joins right after each data gradient anyway).
-hipStream_t wgrad_stream(abd_cnn* net, hipStream_t s) {
-  static const bool on = env_int("ABD_WGRAD_SIDE", 0) != 0;
-  if (!on) return s;
-  if (!net->side) {
-    hipStream_t t = nullptr;
-    if (hipStreamCreateWithFlags(&t, hipStreamNonBlocking) != hipSuccess) return s;
-    if (hipEventCreateWithFlags(&net->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming) != hipSuccess) {
-      (void)hipStreamDestroy(t);
-      return s;
-    }
-    net->side = t;
-  }
-  return net->side;
-}
-
-// everything enqueued on `from` so far happens before what is enqueued on `to` next
-int stream_dep(hipEvent_t ev, hipStream_t from, hipStream_t to) {
-  if (from == to) return 0;
-  ABD_HIP(hipEventRecord(ev, from));
-  ABD_HIP(hipStreamWaitEvent(to, ev, 0));
-  return 0;
-}
-
-// Guarded fallback of the derived BN2 / BN3 backward statistics (bn_any_tiny): the activation pass
-// and its finalize over at most kGuardBlocks blocks, both exiting at once unless a gamma is tiny;
-// they overwrite dgamma / dbeta / bcoef written by the derivation.  w.part is free at this point.
 constexpr int kGuardBlocks = 64;
 int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, double count, const float4* coef,
                  float* dgamma, float* dbeta, BCoef* bcoef, unsigned* ticket, hipStream_t s) {
@@ -4799,13 +3972,12 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
   // fold1: the forward ran conv1_stats_fold_kernel (p1 holds m); conv2's weight gradient is unfolded
   // head: the fused fc head ran its forward and row launches (fc_head.inc); its third launch -- fc
   // gradients, counters, BN3 backward -- replaces everything down to conv3's weight gradient
-  const hipStream_t sw = wgrad_stream(net, s);
   // SyncBN steps take the activation passes: the derived sums' small-gamma fallback (below) is decided
-  // on the device, where the host-issued all-reduce of a second set of sums cannot follow it
-  const bool derive = bn_bwd_derived_on() && !sy.on();
+  // on the device, where the host-issued all-reduce of a second set of sums cannot follow it.
+  // Single-rank steps derive BN2 / BN1's backward sums in the next conv's final weight-gradient
+  // reduction (slab_reduce_derive_kernel).
+  const bool derive = !sy.on();
   int bn3_parts = 0;  // > 0: BN3 backward partials from the fc1 data-gradient epilogue
-  // derived in the weight gradients' last reduction
-  const bool derive_fused = derive;
   const Geo& g = net->g;
   float* G[P_COUNT];
   for (int i = 0; i < P_COUNT; ++i) G[i] = grads + net->off[i];
@@ -4872,9 +4044,8 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     a.drop = drop1;
     a.drop.mask_in = drop1.enabled ? w.mask1 : nullptr;
     // BN3's backward sums in this epilogue (32-column tiles within one channel)
-    static const bool bn3f = env_int("ABD_BN3_FUSED", 1) != 0;
     const int per3 = g.flat / 32;  // columns per BN3 channel (flatten order c, h, w)
-    if (bn3f && !sy.on() && drop1.enabled && per3 % 32 == 0 && env_int("ABD_FC1D_NB", 32) == 32) {
+    if (!sy.on() && drop1.enabled && per3 % 32 == 0) {
       a.part = w.part;
       a.bias = P.p[P_BN3B];
       a.bn_gamma = P.p[P_BN3W];
@@ -4883,16 +4054,10 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       bn3_parts = ((a.M + kBM - 1) / kBM) * (per3 / 32);
     }
     // 32-column tiles: M = B rows is short (4 row tiles at B = 512), so 128-column tiles leave
-    // most CUs idle (96 blocks); ABD_FC1D_NB=128 restores them
-    static const bool nb128 = env_int("ABD_FC1D_NB", 32) == 128;
-    if (drop1.enabled) {
-      if (nb128 ? launch_nt<128, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD)
-                : launch_nt<32, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD))
-        return -1;
-    } else {
-      if (nb128 ? launch_nt<128, EPI_STORE>(a, s, abd::PH_FC1_DGRAD) : launch_nt<32, EPI_STORE>(a, s, abd::PH_FC1_DGRAD))
-        return -1;
-    }
+    // most CUs idle (96 blocks)
+    if (drop1.enabled ? launch_nt<32, EPI_DROPGRAD>(a, s, abd::PH_FC1_DGRAD)
+                      : launch_nt<32, EPI_STORE>(a, s, abd::PH_FC1_DGRAD))
+      return -1;
   }
   }  // !head
   // ---- pool3 / BN3 / relu backward -> dz3; conv3 wgrad + dgrad
@@ -4927,39 +4092,28 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     abd::prof_end(abd::PH_BN3_BWD, s);
     ABD_LAUNCH_CHECK();
     }  // !head
-    if (stream_dep(net->ev_fork, s, sw)) return -1;
-    const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
-    static const bool trw3 = env_int("ABD_WGRAD_TR", 1) != 0;
     int nsl = net->precision == ABD_PREC_BF16
                   ? launch_wgrad_tr<4, 32, 1>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
-                                              abd::PH_CONV3_WGRAD, sw)
-              : (net->precision == ABD_PREC_F32_SPLIT && trw3 && !spw)
-                  ? (env_int("ABD_WGRAD_TR_R3", 4) == 2
-                         ? launch_wgrad_tr<2, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
-                                                  abd::PH_CONV3_WGRAD, sw)
-                         : launch_wgrad_tr<4, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
-                                                  abd::PH_CONV3_WGRAD, sw))
+                                              abd::PH_CONV3_WGRAD, s)
+              : net->precision == ABD_PREC_F32_SPLIT
+                  ? launch_wgrad_tr<4, 32>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, kConv3Slabs, w.slab,
+                                           abd::PH_CONV3_WGRAD, s)
                   : -1;
     if (nsl < 0)
-      nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, env_int("ABD_WGRAD_R3", 4),
-                                      kConv3Slabs, w.slab, abd::PH_CONV3_WGRAD, sw, spw);
+      nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, 4, kConv3Slabs, w.slab,
+                                      abd::PH_CONV3_WGRAD, s);
     // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
     // BN2's backward coefficients come out of the same final reduction (derive_fused)
     const DeriveArgs dv2{nullptr, P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
                          G[P_BN2W], G[P_BN2B], w.bcoef + 64};
-    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], sw, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
-                                derive_fused ? &dv2 : nullptr))
+    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
+                                derive ? &dv2 : nullptr))
       return -1;
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
-    if ((net->precision == ABD_PREC_BF16
-             ? (launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV3_DGRAD) == 0
-                    ? 0
-                    : launch_nt_bf16<64, EPI_STORE, 32>(da, s, abd::PH_CONV3_DGRAD))
-        : net->precision == ABD_PREC_F32_SPLIT
-            ? (launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD) == 0
-                   ? 0
-                   : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV3_DGRAD))
-                                               : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD)))
+    const bool ws3 = net->precision != ABD_PREC_F32 && ws_fits(da);
+    if (ws3 ? (net->precision == ABD_PREC_BF16 ? launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV3_DGRAD)
+                                               : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
+            : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
       return -1;
   }
   // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
@@ -4970,12 +4124,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.dp = w.dp2;
     pa.part = w.part;
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
-    if (derive) {  // conv3's weight / bias gradients (side stream) are final here
-      if (stream_dep(net->ev_join, sw, s) ||
-          (!derive_fused &&
-           bn_bwd_derive(sy, 4, P.p[P_C3W], G[P_C3W], G[P_C3B], 32, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W],
-                         P.p[P_BN2B], w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64, s)))
-        return -1;
+    if (derive) {  // conv3's weight / bias gradients, and BN2's derived sums, are final here
       if (bn_bwd_guard(pa, P.p[P_BN2W], P.p[P_BN2B], (double)B * g.H2 * g.W2, w.coef + 64, G[P_BN2W], G[P_BN2B],
                        w.bcoef + 64, w.tickets + 1, s))
         return -1;
@@ -4999,56 +4148,35 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
-    if (stream_dep(net->ev_fork, s, sw)) return -1;
-    const bool spw = net->precision == ABD_PREC_F32_SPLIT && env_int("ABD_WGRAD_SPLIT", 0) != 0;  // measured slower
-    static const bool trw = env_int("ABD_WGRAD_TR", 1) != 0;
     const WgPlanes wpl{w.dz2s, w.p1s, B * g.H2 * g.W2 * 64, B * g.H1 * g.W1p * 64};
-    int nsl = planes == 3 ? launch_wgrad_tr_planes<2, 3>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                         abd::PH_CONV2_WGRAD, sw, wpl)
-              : planes == 1 ? launch_wgrad_tr_planes<2, 1>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                           abd::PH_CONV2_WGRAD, sw, wpl)
+    int nsl = planes == 1 ? launch_wgrad_tr_planes<2, 1>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                                         abd::PH_CONV2_WGRAD, s, wpl)
               : net->precision == ABD_PREC_BF16
                   ? launch_wgrad_tr<2, 64, 1>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                              abd::PH_CONV2_WGRAD, sw)
-              : (net->precision == ABD_PREC_F32_SPLIT && trw && !spw)
-                  ? (env_int("ABD_WGRAD_TR_R", 2) == 1
-                         ? launch_wgrad_tr<1, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                  abd::PH_CONV2_WGRAD, sw)
-                         : launch_wgrad_tr<2, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
-                                                  abd::PH_CONV2_WGRAD, sw))
+                                              abd::PH_CONV2_WGRAD, s)
+              : net->precision == ABD_PREC_F32_SPLIT
+                  ? launch_wgrad_tr<2, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
+                                           abd::PH_CONV2_WGRAD, s)
                   : -1;
     ABD_CHECK(planes == 0 || nsl >= 0, ABD_E_UNSUPPORTED, "conv2 plane-mode weight gradient geometry");
     if (nsl < 0)
-      nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B,
-                                      spw ? env_int("ABD_WGRAD_R2S", 4) : env_int("ABD_WGRAD_R2", 1),
-                                      kConv2Slabs, w.slab, abd::PH_CONV2_WGRAD, sw, spw);
+      nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, 1, kConv2Slabs, w.slab,
+                                      abd::PH_CONV2_WGRAD, s);
     const DeriveArgs dv1{fold1 ? w.coef : nullptr, P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
                          G[P_BN1W], G[P_BN1B], w.bcoef};
-    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], sw, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]},
-                                derive_fused ? &dv1 : nullptr, fold1 ? w.coef : nullptr))
+    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]},
+                                derive ? &dv1 : nullptr, fold1 ? w.coef : nullptr))
       return -1;
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
-    static const bool mi2d = env_int("ABD_NT_MI2", 0) != 0;
     if (planes > 0) {
       da.srcs = w.dz2s;
       da.splane = B * g.H2 * g.W2 * 64;
     }
-    if ((planes == 3 ? launch_conv_ws_split<EPI_STORE, 3, true>(da, s, abd::PH_CONV2_DGRAD)
-         : planes == 1 ? launch_conv_ws_split<EPI_STORE, 1, true>(da, s, abd::PH_CONV2_DGRAD)
-         : net->precision == ABD_PREC_BF16
-             ? (launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV2_DGRAD) == 0
-                    ? 0
-                    : launch_nt_bf16<64, EPI_STORE, 64>(da, s, abd::PH_CONV2_DGRAD))
-        : net->precision == ABD_PREC_F32_SPLIT
-            ? (split_mi() == 2 ? launch_nt_bf16<64, EPI_STORE, 32, 3, 2>(da, s, abd::PH_CONV2_DGRAD)
-               : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0 ? 0
-               : launch_conv_halo_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD) == 0
-                   ? 0
-               : split_kb() == 16 ? launch_nt_bf16<64, EPI_STORE, 16, 3>(da, s, abd::PH_CONV2_DGRAD)
-                                  : launch_nt_bf16<64, EPI_STORE, 32, 3>(da, s, abd::PH_CONV2_DGRAD))
-        : mi2d ? launch_nt<64, EPI_STORE, 2>(da, s, abd::PH_CONV2_DGRAD)
-        : env_int("ABD_NT_KC64", 0) ? launch_nt<64, EPI_STORE, 1, 64>(da, s, abd::PH_CONV2_DGRAD)
-                                    : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)))
+    const bool ws2 = net->precision != ABD_PREC_F32 && ws_fits(da);
+    if ((planes == 1 ? launch_conv_ws_split<EPI_STORE, 1, true>(da, s, abd::PH_CONV2_DGRAD)
+         : ws2 ? (net->precision == ABD_PREC_BF16 ? launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV2_DGRAD)
+                                                  : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV2_DGRAD))
+               : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV2_DGRAD)))
       return -1;
   }
   // ---- pool1 / BN1 / relu backward fused with the conv1 weight gradient
@@ -5064,12 +4192,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.B = (int)B;
     c1.nblk = (int)nblk_conv1(g, B);
     c1.rows = c1_rows();
-    if (derive) {  // conv2's weight / bias gradients (side stream) are final here
-      if (stream_dep(net->ev_join, sw, s) ||
-          (!derive_fused &&
-           bn_bwd_derive(sy, 5, P.p[P_C2W], G[P_C2W], G[P_C2B], 64, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W],
-                         P.p[P_BN1B], w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, s)))
-        return -1;
+    if (derive) {  // conv2's weight / bias gradients, and BN1's derived sums, are final here
       {
         // guard: (p - beta) / gamma unfolded; folded, the derivation is division-free but routes dy to
         // the window's max / min r, while pool1 picks the first maximum of fl(alpha r + beta') -- the
@@ -5108,7 +4231,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
       ABD_LAUNCH_CHECK();
     }
   }
-  return stream_dep(net->ev_join, sw, s);
+  return 0;
 }
 
 DropArgs make_drop(const abd_train_args* a, int which, uint8_t* ws_mask, int64_t cols) {
@@ -5240,8 +4363,7 @@ int abd_smallcnn_train_step(abd_cnn* net, const abd_train_args* a, void* workspa
     if (loss_and_metrics(net, w, P, a->labels, a->indicators, B, inv, true, a->logprobs_out, nullptr, s)) return -1;
   }
   // single-rank update: conv1's gradient reduction rides on the Adam launch (one launch fewer)
-  static const bool fuse_c1 = env_int("ABD_ADAM_C1", 1) != 0;
-  const bool defer = fuse_c1 && a->do_update && !sy.on() && net->off[P_C1W] == 0 && net->off[P_C1B] == 4 * 64 &&
+  const bool defer = a->do_update && !sy.on() && net->off[P_C1W] == 0 && net->off[P_C1B] == 4 * 64 &&
                      net->off[P_BN1W] == 5 * 64;
   int c1_nblk = 0;
   if (backward(net, w, P, a->grads, a->x, B, d1, s, a->fc_grads_event, sy, a->metrics, fold1, loss_w,

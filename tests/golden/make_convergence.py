@@ -62,7 +62,10 @@ def digest(t: np.ndarray, seed: int, n=64):
     return np.concatenate([[t.sum(), np.sqrt((t * t).sum())], t[idx]])
 
 
-def run(name, out):
+def run(name, out, rng_seed=None):
+    """rng_seed: after the data are built, re-seed torch's CPU generator -- a replicate of the same
+    loop on the same data with other dropout masks and batch orders (the reference's run-to-run
+    variance, SURVEY §7 "Weight-init reproducibility")."""
     c = CONV_CFGS[name]
     torch.manual_seed(c["init_seed"])
     m = ref_models.smallcnn(c["K"], c["lf"])                       # badnets.py:128 (before fix_random)
@@ -70,6 +73,8 @@ def run(name, out):
     opt = torch.optim.Adam(m.parameters(), lr=1e-4)                # :133
     ref_rt.fix_random()                                            # :134
     d = convergence_data(name)                                     # :137 (badnets_poison_data)
+    if rng_seed is not None:
+        torch.manual_seed(rng_seed)
     B = c["B"]
     clean = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(torch.tensor(d["clean_x"]),
                                                                        torch.tensor(d["clean_y"])),
@@ -102,8 +107,9 @@ def run(name, out):
     flat = c["lf"]
     m1 = torch.empty((B, flat)).bernoulli_(0.6).bool()
     m2 = torch.empty((B, 128)).bernoulli_(0.5).bool()
-    for mine, (kept, live) in ((m1, captured[0]), (m2, captured[1])):   # decidable where the input is non-zero
-        assert torch.equal(mine[live], kept[live]), "mask redraw recipe drifted"
+    if rng_seed is None:
+        for mine, (kept, live) in ((m1, captured[0]), (m2, captured[1])):   # decidable where the input is non-zero
+            assert torch.equal(mine[live], kept[live]), "mask redraw recipe drifted"
     out[f"{name}_train"] = np.array(tr, dtype=np.float64)
     out[f"{name}_test"] = np.array(te, dtype=np.float64)
     out[f"{name}_data_digest"] = data_digest(d)
@@ -112,6 +118,9 @@ def run(name, out):
 
 
 SPREAD_THREADS = 3
+# configs whose final ASR is not saturated: also store RNG replicates (<name>_test_seeds: final
+# test() tuple of each, <name>_train_seeds: final train() tuple)
+SEED_REPLICATES = {"flowmur": (1001, 1002, 1003, 1004)}
 
 
 def main():
@@ -136,6 +145,15 @@ def main():
         with torch.backends.mkldnn.flags(enabled=False):
             run(n, alt)
         out[f"{n}_train_alt"], out[f"{n}_test_alt"] = alt[f"{n}_train"], alt[f"{n}_test"]
+        if n in SEED_REPLICATES and os.environ.get("ABD_SKIP_SEEDS") != "1":
+            torch.set_num_threads(min(8, os.cpu_count() or 1))
+            tr_s, te_s = [], []
+            for sd in SEED_REPLICATES[n]:
+                rep = {}
+                run(n, rep, rng_seed=sd)
+                tr_s.append(rep[f"{n}_train"][-1])
+                te_s.append(rep[f"{n}_test"][-1])
+            out[f"{n}_train_seeds"], out[f"{n}_test_seeds"] = np.array(tr_s), np.array(te_s)
         out.pop(f"{n}_train_t3", None)
         out.pop(f"{n}_test_t3", None)
     np.savez_compressed(path, **out)

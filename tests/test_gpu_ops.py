@@ -69,8 +69,8 @@ def test_opcheck_smallcnn_eval(dev):
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     labels = torch.tensor([0, 1, 2, 3], device=dev)
     torch.library.opcheck(torch.ops.abd.smallcnn_eval_metrics.default,
-                          (x, eng.params, eng.running, 10, "f32", labels, None, metrics))
-    y2 = torch.ops.abd.smallcnn_eval_metrics(x, eng.params, eng.running, 10, "f32", labels, None, metrics)
+                          (x, eng.params, eng.running, 10, m.gemm_precision, labels, None, metrics))
+    y2 = torch.ops.abd.smallcnn_eval_metrics(x, eng.params, eng.running, 10, m.gemm_precision, labels, None, metrics)
     assert torch.equal(y2, y) and int(metrics[1]) > 0
 
 

@@ -50,12 +50,18 @@ def _worker(port, attack, q):
         cfg = attack_config(attack)
         B, K, steps = 96, 10, 4
         waves, labels = synth.make_clips_torch(3 * B + 17, cfg.sample_rate, cfg.length, K, seed=41, device=dev)
+        trigger = None
+        if cfg.clean_label:   # FlowMur: target-class clips to poison and a trigger (flowmur.py:67-85)
+            import numpy as np
+            labels[: labels.numel() // 4] = cfg.target_label
+            trigger = (0.05 * np.random.default_rng(1).standard_normal(8000)).astype(np.float32)
 
         def run(dp, sync_bn):
             torch.manual_seed(35)
             model = smallcnn(K, cfg.linear_features).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-            tr = ResidentTrainer(cfg, waves, labels, model, opt, B, seed=35, collectives=dp, sync_bn=sync_bn)
+            tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trigger, seed=35, collectives=dp,
+                                 sync_bn=sync_bn)
             for _ in range(steps):   # crosses the epoch's 17-row tail
                 tr.step()
             m = tr.read_metrics()
