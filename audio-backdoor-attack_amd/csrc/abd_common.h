@@ -30,7 +30,15 @@ void set_last_error(const char* fmt, ...);
   } while (0)
 
 // Launch check: hipGetLastError after an async launch (no sync, graph-capture safe).
+#ifdef ABD_DEBUG_SYNC  // measurement builds only: every launch completes before the next is issued
+#define ABD_LAUNCH_CHECK() \
+  do {                     \
+    ABD_HIP(hipGetLastError()); \
+    ABD_HIP(hipDeviceSynchronize()); \
+  } while (0)
+#else
 #define ABD_LAUNCH_CHECK() ABD_HIP(hipGetLastError())
+#endif
 
 constexpr int kWave = 64;
 

@@ -207,18 +207,20 @@ __device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
 }
 
 // weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets), fc1^T
-constexpr int kGuardTickets = 4;  // BN1, BN2 guard tickets (+ spares)
+constexpr int kGuardTickets = 4;  // BN1, BN2, BN3 guard tickets (+ a spare); the fc head's row tiles follow
 struct PrepArgs {
   const float *c2w, *c3w, *f1w;
   int flat;
   float *w2f, *w2d, *w3f, *w3d, *f1t;
-  unsigned* tickets;  // the step's guard tickets (bn_guard_*_kernel), zeroed here every step
+  unsigned* tickets;  // the step's arrival tickets (guards, head_fwd row tiles), zeroed here every step
+  int ntickets;
 };
 
 __device__ __forceinline__ void prep_weights_body(const PrepArgs& a, int bx, int nb) {
   const int64_t n2 = 64 * 64 * 4, n3 = 32 * 64 * 4, nf = 128LL * a.flat;
   const int64_t total = n2 + n3 + nf;
-  if (bx == 0 && threadIdx.x < kGuardTickets && a.tickets != nullptr) a.tickets[threadIdx.x] = 0u;
+  if (bx == 0 && a.tickets != nullptr)
+    for (int i = threadIdx.x; i < a.ntickets; i += kT) a.tickets[i] = 0u;
   for (int64_t e = bx * (int64_t)kT + threadIdx.x; e < total; e += (int64_t)nb * kT) {
     if (e < n2) {
       const int co = (int)(e / 256), ci = (int)(e / 4 % 64), t = (int)(e % 4);
@@ -525,7 +527,8 @@ struct GuardOut {
   BCoef* bcoef;
   unsigned* ticket;
 };
-__device__ __forceinline__ bool guard_last_block(unsigned* ticket) {
+// the last of n arrivals (n = gridDim.x for the guards, the split count for head_fwd's row tiles)
+__device__ __forceinline__ bool last_arrival(unsigned* ticket, unsigned n) {
   __shared__ unsigned last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -533,7 +536,7 @@ __device__ __forceinline__ bool guard_last_block(unsigned* ticket) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == gridDim.x - 1) ? 1u : 0u;
+    last = (t == n - 1) ? 1u : 0u;
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       // every block has taken its ticket: re-arm it, so a launch that finds no prep block before it
@@ -545,6 +548,8 @@ __device__ __forceinline__ bool guard_last_block(unsigned* ticket) {
   __syncthreads();
   return last != 0u;
 }
+__device__ __forceinline__ bool guard_last_block(unsigned* ticket) { return last_arrival(ticket, gridDim.x); }
+__device__ __forceinline__ bool head_tile_last(unsigned* ticket, unsigned n) { return last_arrival(ticket, n); }
 __device__ __forceinline__ void guard_finalize(const float* part, int nblk, int C, const float* gamma, const GuardOut& g) {
   __shared__ double red[2][kT / kWave];
   for (int c = 0; c < C; ++c) {
@@ -573,13 +578,19 @@ __device__ __forceinline__ void guard_finalize(const float* part, int nblk, int 
   }
 }
 
-// guarded fallback: BN1's statistics from the activations when a gamma is tiny (bn_any_tiny)
-__global__ void __launch_bounds__(kT) conv1_bwd_stats_guard_kernel(C1Args a, const float* gamma, const float* beta,
-                                                                   GuardOut go) {
-  if (!bn_any_tiny(gamma, beta, 64)) return;
-  conv1_bwd_stats_body(a);
-  if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, 64, gamma, go);
-}
+// guarded fallback: BN1's statistics from the activations when a gamma is tiny (bn_any_tiny); runs
+// inside slab_reduce_derive_kernel's launch (a.nblk = that grid)
+struct C1Guard {
+  C1Args a;
+  const float* gamma;
+  const float* beta;
+  GuardOut go;
+  __device__ void operator()() const {
+    if (!bn_any_tiny(gamma, beta, 64)) return;
+    conv1_bwd_stats_body(a);
+    if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, 64, gamma, go);
+  }
+};
 __device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
@@ -1197,8 +1208,8 @@ struct DeriveArgs {
   float* dbeta;
   BCoef* bcoef;
 };
-__global__ void __launch_bounds__(kT) slab_reduce_derive_kernel(const float* slab, int nslab, int Cout, int Ktot,
-                                                                int Cin, float* out, DeriveArgs d) {
+__device__ __forceinline__ void slab_reduce_derive_body(const float* slab, int nslab, int Cout, int Ktot, int Cin,
+                                                        float* out, const DeriveArgs& d) {
   const int c = blockIdx.x;
   const int64_t total = (int64_t)Cout * Ktot;
   // folded source m (BN1 fold): xhat of the pool-selected element is (m - mean) invstd, so
@@ -1388,11 +1399,31 @@ __global__ void __launch_bounds__(kT) bn_pool_fwd_kernel(PoolArgs a) {
 __device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a);
 __global__ void __launch_bounds__(kT) bn_pool_bwd_stats_kernel(PoolArgs a) { bn_pool_bwd_stats_body(a); }
 // guarded fallback: BN2 / BN3 statistics from the activations when a gamma is tiny (bn_any_tiny)
-__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_guard_kernel(PoolArgs a, const float* gamma,
-                                                                     const float* beta, GuardOut go) {
-  if (!bn_any_tiny(gamma, beta, a.C)) return;
-  bn_pool_bwd_stats_body(a);
-  if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, a.C, gamma, go);
+struct PoolGuard {
+  PoolArgs a;
+  const float* gamma;
+  const float* beta;
+  GuardOut go;
+  __device__ void operator()() const {
+    if (!bn_any_tiny(gamma, beta, a.C)) return;
+    bn_pool_bwd_stats_body(a);
+    if (guard_last_block(go.ticket)) guard_finalize(a.part, a.nblk, a.C, gamma, go);
+  }
+};
+struct NoGuard {
+  __device__ void operator()() const {}
+};
+// BN3's guard in its own launch (the separate-backward path's fc1 data-gradient epilogue sums)
+__global__ void __launch_bounds__(kT) bn_pool_bwd_stats_guard_kernel(PoolGuard gd) { gd(); }
+// The derivation's launch carries the guard of the BatchNorm it derives (PoolGuard for BN2, C1Guard
+// for BN1): one block per input channel in both, the guard's partials take gridDim.x slots, and its
+// last block to arrive -- after every block's derived outputs are stored -- overwrites them.  Two
+// launches fewer per step (r4_v1: 4.8 us each, all blocks exiting at the tininess test).
+template <class Guard>
+__global__ void __launch_bounds__(kT) slab_reduce_derive_kernel(const float* slab, int nslab, int Cout, int Ktot,
+                                                                int Cin, float* out, DeriveArgs d, Guard gd) {
+  slab_reduce_derive_body(slab, nslab, Cout, Ktot, Cin, out, d);
+  gd();
 }
 __device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a) {
   const int CG = a.C / 4;
@@ -2026,12 +2057,15 @@ constexpr int kDmaSpan = 64;  // staged positions per tile and group (span <= 31
 #ifndef ABD_DMA_ABL  // ablation bits (measurement builds only; results wrong): 1 no epilogue stores,
 #define ABD_DMA_ABL 0  // 2 no DMA waits, 4 no DMA, 8 no A split
 #endif
-#ifndef ABD_DMA_SPREAD  // A/B: the DMA refill spread over taps 1-3 (1) or issued at tap 1 (0)
-#define ABD_DMA_SPREAD 0
-#endif
-template <int EPI, int NP, int NJ = 2>
+// PA (bf16 mode's plane operands, NP = 1): the A source is the producer's bf16 plane (NTArgs::srcs,
+// store_planes4), staged as 32 B per position and group (two lanes per position, 32 positions per
+// DMA instruction: half the instructions and bytes of the fp32 staging), the 16-B half a lane reads
+// XOR-swizzled by (position >> 3) & 1, and read straight into the MFMA operand (no split).
+template <int EPI, int NP, int NJ = 2, bool PA = false>
 __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
+  static_assert(!PA || NP == 1, "pre-split staging: the single bf16 plane");
   constexpr int CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
+  constexpr int PPI = PA ? 32 : 16;  // staged positions per DMA instruction
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
   __shared__ __attribute__((aligned(16))) float stage[WPB][kDmaSpan * 16];
   __shared__ float red[WPB][N][2];
@@ -2071,8 +2105,11 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
     tmin = min(tmin, tofs[t]);
     tmax = max(tmax, tofs[t]);
   }
-  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
+  const __amdgpu_buffer_rsrc_t arsrc =
+      PA ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.srcs), 0,
+                                             (int)std::min<int64_t>((int64_t)npos * CS * 2, 0x7ffffff0), 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.src), 0,
+                                             (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
   const int kq = 8 * (lane >> 5);
   float st[NJ][2];
   float bias[NJ];
@@ -2090,16 +2127,23 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   // only the 16-position blocks the tile reads (need: wave-uniform; typically 48 of the 64 slots)
   auto dma1 = [&](int p0, int cg, int need, int i) {
     if (ABD_DMA_ABL & 4) return;
-    if (i > 0 && 16 * i >= need) return;
-    const int pos = 16 * i + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
-    const uint32_t off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
+    if (i > 0 && PPI * i >= need) return;
+    uint32_t off;
+    if constexpr (PA) {  // PA: instruction i, lane l -> position 32 i + l / 2, half (l % 2) ^ ((pos >> 3) & 1)
+      const int pos = 32 * i + (lane >> 1);
+      const int half = (lane & 1) ^ ((pos >> 3) & 1);
+      off = (uint32_t)(((p0 + pos) * CS + cg * 16 + half * 8) * 2);
+    } else {
+      const int pos = 16 * i + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((pos >> 2) & 3);
+      off = (uint32_t)(((p0 + pos) * CS + cg * 16 + chunk * 4) * 4);  // past the end: zeros
+    }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (__attribute__((address_space(3))) void*)(sw + i * 256), 16,
                                              (int)off, 0, 0, 0);
   };
   auto dma = [&](int p0, int cg, int need) {
 #pragma unroll
-    for (int i = 0; i < kDmaSpan / 16; ++i) dma1(p0, cg, need, i);
+    for (int i = 0; i < kDmaSpan / PPI; ++i) dma1(p0, cg, need, i);
   };
   const int ntiles = (r_hi - r_lo + 31) / 32;
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -2181,10 +2225,15 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);  // an invalid tap's position is clamped
-        const int sx = (pos >> 2) & 3;
-        const float* rowp = sw + pos * 16;
-        raw[t][0] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5)) ^ sx) * 4));
-        raw[t][1] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5) + 1) ^ sx) * 4));
+        if constexpr (PA) {
+          const char* rowp = reinterpret_cast<const char*>(sw) + pos * 32;
+          raw[t][0] = raw[t][1] = *reinterpret_cast<const uint4*>(rowp + (((lane >> 5) ^ ((pos >> 3) & 1)) * 16));
+        } else {
+          const int sx = (pos >> 2) & 3;
+          const float* rowp = sw + pos * 16;
+          raw[t][0] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5)) ^ sx) * 4));
+          raw[t][1] = *reinterpret_cast<const uint4*>(rowp + (((2 * (lane >> 5) + 1) ^ sx) * 4));
+        }
         if constexpr (EPI != EPI_CONV) {  // and zeroed (forward taps never leave the grid)
           if (!((tm >> t) & 1u)) raw[t][0] = raw[t][1] = make_uint4(0u, 0u, 0u, 0u);
         }
@@ -2197,19 +2246,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
           // the next tile's group 0
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        if (ABD_DMA_SPREAD) {
-          // the refill's instructions spread over taps 1-3 (instruction i at tap 1 + i, the 4th with
-          // the 3rd): each tap's MFMAs carry one DMA issue instead of tap 1 carrying all of them
-          if (t >= 1) {
-            if (cg + 1 < G) {
-              dma1(p0, cg + 1, need, t - 1);
-              if (t == 3) dma1(p0, cg + 1, need, 3);
-            } else if (more) {
-              dma1(p0n, 0, needn, t - 1);
-              if (t == 3) dma1(p0n, 0, needn, 3);
-            }
-          }
-        } else if (t == 1) {
+        if (t == 1) {
           if (cg + 1 < G) dma(p0, cg + 1, need);
           else if (more) dma(p0n, 0, needn);
         }
@@ -2217,7 +2254,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
         // next step's B fragments (past the tile's last step: the next tile's first)
         load_b(((s + 1) % (4 * G)) / 4, (s + 1) % 4, bvs[(s + 1) & 1]);
         bf16x8 av[NP];
-        if (ABD_DMA_ABL & 8) {
+        if constexpr (PA) {
+          av[0] = __builtin_bit_cast(bf16x8, raw[t][0]);
+        } else if (ABD_DMA_ABL & 8) {
 #pragma unroll
           for (int q = 0; q < NP; ++q) av[q] = __builtin_bit_cast(bf16x8, q == 1 ? raw[t][1] : raw[t][0]);
         } else {
@@ -3027,7 +3066,8 @@ struct Work {
   float* daT;              // fused fc head: da transposed (128 x B), head_dgrad's A operand
   uint16_t* p1s;           // conv2 plane mode: pool1 output m as exact bf16 planes [3][n_p1]
   uint16_t* dz2s;          // conv2 plane mode: BN2-backward output dz2 as planes [3][n_r2]
-  unsigned* tickets;       // guarded BN fallbacks' arrival tickets (zeroed by the prep blocks)
+  unsigned* tickets;       // guarded BN fallbacks' and head_fwd's arrival tickets (zeroed by the prep blocks)
+  int ntickets;
   float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
   double* ft2;             //   and the beta' bias terms [ci][co]
   float* slab;
@@ -3161,7 +3201,8 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   }
   w.p1s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_p1 * sizeof(uint16_t)));
   w.dz2s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_r2 * sizeof(uint16_t)));
-  w.tickets = reinterpret_cast<unsigned*>(take(kGuardTickets * sizeof(unsigned)));
+  w.ntickets = kGuardTickets + (int)((B + 31) / 32);
+  w.tickets = reinterpret_cast<unsigned*>(take((size_t)w.ntickets * sizeof(unsigned)));
   w.bytes = off;
   return w;
 }
@@ -3177,7 +3218,7 @@ Params params_of(const abd_cnn* net, const float* flat) {
 }
 
 PrepArgs prep_args(const Params& P, const Work& w, const Geo& g) {
-  return PrepArgs{P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t, w.tickets};
+  return PrepArgs{P.p[P_C2W], P.p[P_C3W], P.p[P_F1W], g.flat, w.w2f, w.w2d, w.w3f, w.w3d, w.f1t, w.tickets, w.ntickets};
 }
 unsigned prep_blocks(const Geo& g) { return (unsigned)grid_for(64 * 256 + 32 * 256 + 128LL * g.flat); }
 
@@ -3277,10 +3318,11 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.n_w1 = 4 * ((g.flat + 31) / 32);
   a.n_w2 = 4 * ((g.K + 31) / 32) + (g.K + 128 + kHeadW2 - 1) / kHeadW2;  // fc2 weight tiles + bias sums
   a.n_apply = head_napply(a.pool, B);
+  a.tickets = w.tickets + kGuardTickets;
   return a;
 }
 
-// launch 1 (forward: pool3 + dropout1 + fc1 partials) / 2 (row head, then dp3 + BN3 sums) /
+// launch 1 (forward: pool3 + dropout1 + fc1 partials, the row head in each tile's last block) / 2 (dp3 + BN3 sums) /
 // 3 (gradients + BN3 apply)
 int launch_head(int which, const HeadArgs& a, hipStream_t s) {
   if (which == 1) {
@@ -3293,10 +3335,6 @@ int launch_head(int which, const HeadArgs& a, hipStream_t s) {
     else head_fwd_kernel<8><<<grid, kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_FWD, s);
   } else if (which == 2) {
-    abd::prof_begin(abd::PH_HEAD_MID, s);
-    head_row_kernel<<<(unsigned)((a.B + kHeadRows - 1) / kHeadRows), kT, 0, s>>>(a);
-    abd::prof_end(abd::PH_HEAD_MID, s);
-    ABD_LAUNCH_CHECK();
     abd::prof_begin(abd::PH_HEAD_DGRAD, s);
     head_dgrad_kernel<<<dim3((unsigned)a.nft, (unsigned)a.nrb), kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_DGRAD, s);
@@ -3591,10 +3629,12 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
   const bool dg_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == -1 && a.dh[2] == -1 && a.dw[2] == 0 &&
                        a.dh[3] == -1 && a.dw[3] == -1;
-  // conv3 (N = 32) through the same kernel with one 32-column tile per wave
-  if (!PA && dma && (a.N == 64 || a.N == 32) && a.Cs == 64 &&
+  // conv3 (N = 32) through the same kernel with one 32-column tile per wave; bf16's plane operands
+  // (PA, conv2) staged as bf16
+  if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
-    if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
+    if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_dma_kernel<EPI, NP, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
     if (ko) conv_ws_split_kernel<EPI, 2, 64, 1, 8, 8, NP, true, true><<<dim3(nb), dim3(512), 0, s>>>(a);
@@ -3637,8 +3677,11 @@ int launch_nt(const NTArgs& a, hipStream_t s, int phase) {
 // dv != nullptr (conv weight gradients): the final reduction also derives the BatchNorm feeding the
 // conv (slab_reduce_derive_kernel)
 // fold (conv2 under the BN1 fold): the gradient is unfolded with the bias gradient bias.out
+// gd: the small-gamma guard riding on the derivation (its partial count must be conv_cin, the grid)
+template <class Guard = NoGuard>
 int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* out, hipStream_t s,
-                 BiasSum bias = BiasSum{}, const DeriveArgs* dv = nullptr, const float4* fold = nullptr) {
+                 BiasSum bias = BiasSum{}, const DeriveArgs* dv = nullptr, const float4* fold = nullptr,
+                 Guard gd = Guard{}) {
   const int64_t total = (int64_t)N * Ktot;
   const float* src = w.slab;
   int n = nsl;
@@ -3657,7 +3700,7 @@ int reduce_slabs(const Work& w, int nsl, int N, int Ktot, int conv_cin, float* o
     n = G;
   }
   if (dv != nullptr && conv_cin > 0)
-    slab_reduce_derive_kernel<<<conv_cin, kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, *dv);
+    slab_reduce_derive_kernel<Guard><<<conv_cin, kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, *dv, gd);
   else
     slab_reduce_kernel<<<grid_for(total), kT, 0, s>>>(src, n, N, Ktot, conv_cin, out, fold, bias.out);
   ABD_LAUNCH_CHECK();
@@ -3958,7 +4001,8 @@ int bn_bwd_guard(const PoolArgs& pa_in, const float* gamma, const float* beta, d
                  float* dgamma, float* dbeta, BCoef* bcoef, unsigned* ticket, hipStream_t s) {
   PoolArgs pa = pa_in;
   pa.nblk = std::min(grid_for((int64_t)pa.B * pa.Ho * pa.Wo * pa.C / 4), kGuardBlocks);
-  bn_pool_bwd_stats_guard_kernel<<<pa.nblk, kT, 0, s>>>(pa, gamma, beta, GuardOut{count, coef, dgamma, dbeta, bcoef, ticket});
+  bn_pool_bwd_stats_guard_kernel<<<pa.nblk, kT, 0, s>>>(
+      PoolGuard{pa, gamma, beta, GuardOut{count, coef, dgamma, dbeta, bcoef, ticket}});
   ABD_LAUNCH_CHECK();
   return 0;
 }
@@ -4102,21 +4146,34 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (nsl < 0)
       nsl = launch_wgrad_rows<32, 64>(w.dz3, w.p2, g.H3, g.W3, g.H2p, g.W2p, B, 4, kConv3Slabs, w.slab,
                                       abd::PH_CONV3_WGRAD, s);
-    // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
-    // BN2's backward coefficients come out of the same final reduction (derive_fused)
-    const DeriveArgs dv2{nullptr, P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
-                         G[P_BN2W], G[P_BN2B], w.bcoef + 64};
-    if (nsl < 0 || reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
-                                derive ? &dv2 : nullptr))
-      return -1;
+    // conv3's data gradient first: the BN2 guard riding on the reduction below reads dp2
     NTArgs da = conv_dgrad_args(w.dz3, g.H3, g.W3, 32, g.H2p, g.W2p, B, w.w3d, 64, w.dp2);
     const bool ws3 = net->precision != ABD_PREC_F32 && ws_fits(da);
     if (ws3 ? (net->precision == ABD_PREC_BF16 ? launch_conv_ws_split<EPI_STORE, 1>(da, s, abd::PH_CONV3_DGRAD)
                                                : launch_conv_ws_split<EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
             : launch_nt<64, EPI_STORE>(da, s, abd::PH_CONV3_DGRAD))
       return -1;
+    // conv3 bias gradient (BN3-backward partials) rides on the slab reduction's launch
+    // BN2's backward coefficients come out of the same final reduction (derive_fused), with BN2's
+    // small-gamma guard (PoolGuard: one partial per derivation block)
+    const DeriveArgs dv2{nullptr, P.p[P_C3W], G[P_C3B], P.p[P_BN2W], P.p[P_BN2B], w.coef + 64, (double)B * g.H2 * g.W2,
+                         G[P_BN2W], G[P_BN2B], w.bcoef + 64};
+    PoolArgs pg = pool_args(g, 2, B);
+    pg.r = w.r2;
+    pg.coef = w.coef + 64;
+    pg.dp = w.dp2;
+    pg.part = w.part;
+    pg.nblk = 64;  // = reduce_slabs' conv_cin (the derivation grid)
+    const PoolGuard guard2{pg, P.p[P_BN2W], P.p[P_BN2B],
+                           GuardOut{(double)B * g.H2 * g.W2, w.coef + 64, G[P_BN2W], G[P_BN2B], w.bcoef + 64,
+                                    w.tickets + 1}};
+    if (nsl < 0 || (derive ? reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]},
+                                          &dv2, nullptr, guard2)
+                           : reduce_slabs(w, nsl, 32, 256, 64, G[P_C3W], s, BiasSum{w.partb3, pa.nblk, 32, G[P_C3B]})))
+      return -1;
   }
   // ---- pool2 / BN2 / relu backward -> dz2; conv2 wgrad + dgrad
+  int nsl2 = -1, pa_nblk2 = 0;  // conv2's weight-gradient slabs and bias partials (reduced with BN1 below)
   {
     PoolArgs pa = pool_args(g, 2, B);
     pa.r = w.r2;
@@ -4124,11 +4181,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     pa.dp = w.dp2;
     pa.part = w.part;
     pa.nblk = grid_for(B * pa.Ho * pa.Wo * 64 / 4);
-    if (derive) {  // conv3's weight / bias gradients, and BN2's derived sums, are final here
-      if (bn_bwd_guard(pa, P.p[P_BN2W], P.p[P_BN2B], (double)B * g.H2 * g.W2, w.coef + 64, G[P_BN2W], G[P_BN2B],
-                       w.bcoef + 64, w.tickets + 1, s))
-        return -1;
-    } else {
+    if (!derive) {  // derived: conv3's weight / bias gradients, BN2's sums and its guard are final here
       bn_pool_bwd_stats_kernel<<<pa.nblk, kT, 0, s>>>(pa);
       ABD_LAUNCH_CHECK();
       if (bn_bwd_finalize(sy, 4, w.part, pa.nblk, 64, (double)B * g.H2 * g.W2, P.p[P_BN2W], w.coef + 64, G[P_BN2W],
@@ -4148,6 +4201,7 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     bn_bwd_apply_kernel<<<pa.nblk, kT, 0, s>>>(pa, win_ext_h(pa), win_ext_w(pa));
     abd::prof_end(abd::PH_BN2_BWD, s);
     ABD_LAUNCH_CHECK();
+    pa_nblk2 = pa.nblk;
     const WgPlanes wpl{w.dz2s, w.p1s, B * g.H2 * g.W2 * 64, B * g.H1 * g.W1p * 64};
     int nsl = planes == 1 ? launch_wgrad_tr_planes<2, 1>(g.H2, g.W2, g.H1, g.W1p, B, kConv2Slabs, w.slab,
                                                          abd::PH_CONV2_WGRAD, s, wpl)
@@ -4162,11 +4216,8 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     if (nsl < 0)
       nsl = launch_wgrad_rows<64, 64>(w.dz2, w.p1, g.H2, g.W2, g.H1, g.W1p, B, 1, kConv2Slabs, w.slab,
                                       abd::PH_CONV2_WGRAD, s);
-    const DeriveArgs dv1{fold1 ? w.coef : nullptr, P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
-                         G[P_BN1W], G[P_BN1B], w.bcoef};
-    if (nsl < 0 || reduce_slabs(w, nsl, 64, 256, 64, G[P_C2W], s, BiasSum{w.partb2, pa.nblk, 64, G[P_C2B]},
-                                derive ? &dv1 : nullptr, fold1 ? w.coef : nullptr))
-      return -1;
+    nsl2 = nsl;
+    // conv2's data gradient first: the BN1 guard riding on the reduction below reads dp1
     NTArgs da = conv_dgrad_args(w.dz2, g.H2, g.W2, 64, g.H1, g.W1p, B, w.w2d, 64, w.dp1);
     if (planes > 0) {
       da.srcs = w.dz2s;
@@ -4192,20 +4243,25 @@ int backward(abd_cnn* net, const Work& w, const Params& P, float* grads, const f
     c1.B = (int)B;
     c1.nblk = (int)nblk_conv1(g, B);
     c1.rows = c1_rows();
-    if (derive) {  // conv2's weight / bias gradients, and BN1's derived sums, are final here
-      {
-        // guard: (p - beta) / gamma unfolded; folded, the derivation is division-free but routes dy to
-        // the window's max / min r, while pool1 picks the first maximum of fl(alpha r + beta') -- the
-        // same element unless alpha is so small that the rounded values tie (at gamma = 0 every
-        // window ties and the reference routes to its first element)
-        C1Args c1g = c1;
-        c1g.nblk = (int)std::min<int64_t>(c1.nblk, kGuardBlocks);
-        conv1_bwd_stats_guard_kernel<<<c1g.nblk, kT, 0, s>>>(
-            c1g, P.p[P_BN1W], P.p[P_BN1B],
-            GuardOut{(double)B * g.H1 * g.W1, w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, w.tickets + 0});
-        ABD_LAUNCH_CHECK();
-      }
+    const DeriveArgs dv1{fold1 ? w.coef : nullptr, P.p[P_C2W], G[P_C2B], P.p[P_BN1W], P.p[P_BN1B], w.coef, (double)B * g.H1 * g.W1,
+                         G[P_BN1W], G[P_BN1B], w.bcoef};
+    if (derive) {
+      // conv2's weight / bias gradients, BN1's derived sums and its small-gamma guard in one launch.
+      // Guard: (p - beta) / gamma unfolded; folded, the derivation is division-free but routes dy to
+      // the window's max / min r, while pool1 picks the first maximum of fl(alpha r + beta') -- the
+      // same element unless alpha is so small that the rounded values tie (at gamma = 0 every window
+      // ties and the reference routes to its first element)
+      C1Args c1g = c1;
+      c1g.nblk = 64;  // = reduce_slabs' conv_cin (the derivation grid)
+      const C1Guard guard1{c1g, P.p[P_BN1W], P.p[P_BN1B],
+                           GuardOut{(double)B * g.H1 * g.W1, w.coef, G[P_BN1W], G[P_BN1B], w.bcoef, w.tickets + 0}};
+      if (nsl2 < 0 || reduce_slabs(w, nsl2, 64, 256, 64, G[P_C2W], s, BiasSum{w.partb2, pa_nblk2, 64, G[P_C2B]}, &dv1,
+                                  fold1 ? w.coef : nullptr, guard1))
+        return -1;
     } else {
+      if (nsl2 < 0 || reduce_slabs(w, nsl2, 64, 256, 64, G[P_C2W], s, BiasSum{w.partb2, pa_nblk2, 64, G[P_C2B]}, nullptr,
+                                  fold1 ? w.coef : nullptr))
+        return -1;
       conv1_bwd_stats_kernel<<<c1.nblk, kT, 0, s>>>(c1);
       ABD_LAUNCH_CHECK();
       if (bn_bwd_finalize(sy, 5, w.part, c1.nblk, 64, (double)B * g.H1 * g.W1, P.p[P_BN1W], w.coef, G[P_BN1W],

@@ -121,6 +121,11 @@ SPREAD_THREADS = 3
 # configs whose final ASR is not saturated: also store RNG replicates (<name>_test_seeds: final
 # test() tuple of each, <name>_train_seeds: final train() tuple)
 SEED_REPLICATES = {"flowmur": (1001, 1002, 1003, 1004)}
+# chaotic configs: further fp32 implementations of the SAME run (same seed, data and masks; other
+# summation orders: oneDNN on / off x thread counts), stored as <name>_finalalt<j>_<param> and
+# <name>_test_alt<j>, j = 2, 3, ... -- one alternative underestimates the implementation spread of
+# final parameters that the reference's own run amplifies chaotically
+ALT_EXTRA = {"flowmur": ((True, 1), (False, 8), (True, 5))}
 
 
 def main():
@@ -136,15 +141,31 @@ def main():
     path = os.path.join(HERE, "convergence_ref.npz")
     out = dict(np.load(path)) if os.path.exists(path) else {}
     only_alt = os.environ.get("ABD_ONLY_ALT") == "1"
+    only_extra = os.environ.get("ABD_ONLY_EXTRA") == "1"   # just the ALT_EXTRA implementations
     for n in names:
-        if not only_alt:
+        if not only_alt and not only_extra:
             torch.set_num_threads(min(8, os.cpu_count() or 1))
             run(n, out)
-        torch.set_num_threads(SPREAD_THREADS)
-        alt = {}
-        with torch.backends.mkldnn.flags(enabled=False):
-            run(n, alt)
-        out[f"{n}_train_alt"], out[f"{n}_test_alt"] = alt[f"{n}_train"], alt[f"{n}_test"]
+        if not only_extra:
+            torch.set_num_threads(SPREAD_THREADS)
+            alt = {}
+            with torch.backends.mkldnn.flags(enabled=False):
+                run(n, alt)
+            out[f"{n}_train_alt"], out[f"{n}_test_alt"] = alt[f"{n}_train"], alt[f"{n}_test"]
+            for k, v in alt.items():   # final-parameter digests of the second implementation
+                if k.startswith(f"{n}_final_"):
+                    out[k.replace(f"{n}_final_", f"{n}_finalalt_")] = v
+        for j, (mk, thr) in enumerate(ALT_EXTRA.get(n, ()), start=2):
+            torch.set_num_threads(thr)
+            alt = {}
+            with torch.backends.mkldnn.flags(enabled=mk):
+                run(n, alt)
+            out[f"{n}_test_alt{j}"] = alt[f"{n}_test"]
+            for k, v in alt.items():
+                if k.startswith(f"{n}_final_"):
+                    out[k.replace(f"{n}_final_", f"{n}_finalalt{j}_")] = v
+        if only_extra:
+            continue
         if n in SEED_REPLICATES and os.environ.get("ABD_SKIP_SEEDS") != "1":
             torch.set_num_threads(min(8, os.cpu_count() or 1))
             tr_s, te_s = [], []

@@ -156,28 +156,35 @@ def test_replay_matches_reference_epochs(dev, conv_ref, name, prec):
     for col in (0, 1):
         allowed = final_allowed(conv_ref, name, col, "torch_cpu")
         assert abs(te[-1, col] - rte[-1, col]) <= allowed, (col, te[-1], rte[-1], allowed)
-    # final parameters: same model up to the same fp32 drift (norms within 1 %)
+    # final parameters: same model up to the same fp32 drift (norms within 1 %, or 3x the widest gap
+    # of the reference's other fp32 implementations where that is wider: flowmur's chaotic run,
+    # make_convergence.py ALT_EXTRA)
     from test_oracle_golden import _digest
     sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     for k, v in sd.items():
         if k.endswith("num_batches_tracked"):
             continue
         ref = conv_ref[f"{name}_final_{k}"]
-        assert abs(_digest(v, 21)[1] - ref[1]) <= 1e-2 * abs(ref[1]), k
+        alts = [conv_ref[a] for a in [f"{name}_finalalt_{k}"] + [f"{name}_finalalt{j}_{k}" for j in range(2, 8)]
+                if a in conv_ref]
+        gap = max([abs(a[1] - ref[1]) for a in alts], default=0.0)
+        tol = max(1e-2 * abs(ref[1]), 3.0 * gap)
+        assert abs(_digest(v, 21)[1] - ref[1]) <= tol, (k, _digest(v, 21)[1], ref[1], tol)
 
 
 def final_allowed(conv_ref, name, col, source):
     """Allowed |GPU - reference| (pp) of the final clean accuracy (col 0) / ASR (col 1).
 
     The north_star's 0.5 pp, widened only by what the REFERENCE ITSELF cannot hold: with the
-    reference's own dropout masks and batch orders (source 'torch_cpu') its gap to its second fp32
-    implementation (native convolutions, ``*_test_alt``); with device dropout -- other masks and
+    reference's own dropout masks and batch orders (source 'torch_cpu') its widest gap to its other
+    fp32 implementations (native convolutions, ``*_test_alt``; thread counts, ``*_test_alt<j>``); with device dropout -- other masks and
     orders, i.e. another draw of the run -- the range of the reference's final metric over its
     RNG replicates (``*_test_seeds``: the same loop and data under other torch seeds,
     make_convergence.py SEED_REPLICATES).  For the saturated configs both are 0 and the bound is
     0.5 pp; flowmur's clean-label ASR is not saturated (DESIGN.md §4 lists the numbers)."""
     ref = conv_ref[f"{name}_test"][-1, col]
-    spread = abs(conv_ref[f"{name}_test_alt"][-1, col] - ref)
+    spread = max(abs(conv_ref[a][-1, col] - ref) for a in [f"{name}_test_alt"] +
+                 [f"{name}_test_alt{j}" for j in range(2, 8)] if a in conv_ref)
     if source == "device" and f"{name}_test_seeds" in conv_ref:
         seeds = conv_ref[f"{name}_test_seeds"][:, col]
         spread = max(spread, float(np.max(np.abs(seeds - ref))))

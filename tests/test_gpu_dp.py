@@ -121,6 +121,12 @@ def _equiv_worker(rank, world, port, q):
         B, K, steps = 64, 10, 3
         waves, labels = synth.make_clips_torch(256, cfg.sample_rate, cfg.length, K, seed=35, device=dev)
 
+        # the 1-rank reference runs the same data-parallel code path (SyncBN over a one-rank group:
+        # no BN1 fold, the activation passes for the BN sums, the unfused fc head): the fused
+        # single-rank path differs from it in fp32 rounding, which Adam's sign-like first steps turn
+        # into +-lr parameter differences
+        solo = dist.new_group([0])
+
         def run(world_, rank_, pg_world):
             # rank 1 seeded differently (the seed + rank pattern): parameters, BN buffers AND the
             # dropout seed come from rank 0, so the run still equals the 1-rank run
@@ -128,7 +134,7 @@ def _equiv_worker(rank, world, port, q):
             model = smallcnn(K, cfg.linear_features).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
             tr = ResidentTrainer(cfg, waves, labels, model, opt, B // world_, seed=35, rank=rank_, world=world_,
-                                 sync_bn=world_ > 1)
+                                 sync_bn=True, collectives=True, process_group=None if world_ > 1 else solo)
             for _ in range(steps):
                 tr.step()
             m = tr.read_metrics()
@@ -202,12 +208,14 @@ def _tail_worker(rank, world, port, q, N):
         G, K = 64, 10
         waves, labels = synth.make_clips_torch(N, cfg.sample_rate, cfg.length, K, seed=36, device=dev)
 
+        solo = dist.new_group([0])   # the 1-rank reference on the same (SyncBN) code path
+
         def run(world_, rank_):
             torch.manual_seed(35)
             model = smallcnn(K, cfg.linear_features).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
             tr = ResidentTrainer(cfg, waves, labels, model, opt, G // world_, seed=35, rank=rank_, world=world_,
-                                 sync_bn=world_ > 1)
+                                 sync_bn=True, collectives=True, process_group=None if world_ > 1 else solo)
             steps = tr.steps_per_epoch()
             m = tr.run_epoch()
             tr.sync_buffers()

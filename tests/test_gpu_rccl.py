@@ -11,8 +11,10 @@ RCCL group drives every collective of ResidentTrainer's data-parallel step (coll
   stream between two of its launches;
 * reduce_metrics / broadcast_state (the initial parameter, buffer and dropout-seed broadcast).
 
-Parameters, BN buffers and the epoch metrics must equal the plain one-process step's (1e-6; the
-DP step runs other launches: no BN1 fold, SyncBN's unfused head, Adam after the all-reduce).
+Parameters, BN buffers and the epoch metrics must equal (1e-6) the plain one-process step's for the
+collectives-only step (the same kernels, Adam after the all-reduce), and the same SyncBN step run
+over a one-rank gloo group for the SyncBN step (SyncBN has its own launches: no BN1 fold, the
+activation passes, the unfused fc head).
 """
 import os
 import socket
@@ -56,12 +58,14 @@ def _worker(port, attack, q):
             labels[: labels.numel() // 4] = cfg.target_label
             trigger = (0.05 * np.random.default_rng(1).standard_normal(8000)).astype(np.float32)
 
-        def run(dp, sync_bn):
+        gloo = dist.new_group([0], backend="gloo")
+
+        def run(dp, sync_bn, pg=None):
             torch.manual_seed(35)
             model = smallcnn(K, cfg.linear_features).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
             tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=trigger, seed=35, collectives=dp,
-                                 sync_bn=sync_bn)
+                                 sync_bn=sync_bn, process_group=pg)
             for _ in range(steps):   # crosses the epoch's 17-row tail
                 tr.step()
             m = tr.read_metrics()
@@ -70,9 +74,14 @@ def _worker(port, attack, q):
             eng = model._engine
             return eng.params.clone(), eng.running.clone(), eng.nbt.clone(), m, tr
 
-        p0, r0, n0, m0, _ = run(False, False)
+        # collectives only: against the plain single-rank step (the same kernels)
+        # SyncBN: against the same SyncBN step over a one-rank gloo group (the SyncBN path has its own
+        # kernels -- no BN1 fold, activation passes -- so the reference is that path, not the fused one)
+        plain = run(False, False)
+        gloo_sync = run(True, True, gloo)
         res = {"backend": dist.get_backend()}
         for sync_bn in (False, True):
+            p0, r0, n0, m0, _ = gloo_sync if sync_bn else plain
             p1, r1, n1, m1, tr = run(True, sync_bn)
             nrel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
             res[sync_bn] = {"params": nrel(p1, p0), "running": nrel(r1, r0), "nbt": torch.equal(n1, n0),
