@@ -679,6 +679,14 @@ __device__ __forceinline__ f2v cmulv(f2v a, f2v w) {
 // one-sided negation into VOP3P modifiers and spends a v_pk_add + v_pk_mov building (-w.y, w.x)
 // (4 instructions); written out it is one v_pk_mul + one v_pk_fma with op_sel / neg modifiers:
 //   t = (a.x w.x, a.x w.y);  r.lo = -a.y w.y + t.lo,  r.hi = a.y w.x + t.hi   (conj: signs of a.y flip)
+#ifdef ABD_NO_PK  // the packed-FP32-free build (Makefile libabd_nopk.so): the same roundings, lane by lane
+__device__ __forceinline__ f2v cmul_rt(f2v a, f2v w) {
+  return f2v{__builtin_fmaf(-a.y, w.y, a.x * w.x), __builtin_fmaf(a.y, w.x, a.x * w.y)};
+}
+__device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
+  return f2v{__builtin_fmaf(a.y, w.y, a.x * w.x), __builtin_fmaf(-a.y, w.x, a.x * w.y)};
+}
+#else
 __device__ __forceinline__ f2v cmul_rt(f2v a, f2v w) {
   f2v t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
@@ -693,6 +701,7 @@ __device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
       : "=v"(r) : "v"(a), "v"(w), "v"(t));
   return r;
 }
+#endif
 // value the compiler must treat as defined without materialising it (skip paths of the
 // wave-uniform pass guards: otherwise the backend zero-fills every register of the butterfly)
 // An opaque unspecified value.  (freeze(poison) -- __builtin_nondeterministic_value -- removes the
