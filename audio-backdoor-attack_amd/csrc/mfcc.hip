@@ -675,33 +675,17 @@ __device__ __forceinline__ f2v cmulv(f2v a, f2v w) {
   const f2v ax = __builtin_shufflevector(a, a, 0, 0), ay = __builtin_shufflevector(a, a, 1, 1);
   return fmav(ay, __builtin_shufflevector(w, -w, 3, 0), ax * w);
 }
-// a * w and conj(a) * w for run-time w (table twiddles, chirps): the backend cannot fold the
-// one-sided negation into VOP3P modifiers and spends a v_pk_add + v_pk_mov building (-w.y, w.x)
-// (4 instructions); written out it is one v_pk_mul + one v_pk_fma with op_sel / neg modifiers:
+// a * w and conj(a) * w for run-time w (table twiddles, chirps), lane by lane:
 //   t = (a.x w.x, a.x w.y);  r.lo = -a.y w.y + t.lo,  r.hi = a.y w.x + t.hi   (conj: signs of a.y flip)
-#ifdef ABD_NO_PK  // the packed-FP32-free build (Makefile libabd_nopk.so): the same roundings, lane by lane
+// The library is built without packed-FP32 instructions (Makefile, PKFLAGS): round 3's v_pk_mul /
+// v_pk_fma pair with op_sel modifiers gave the same roundings, and the scalar build measured no
+// slower (r4: STFT 0.249 vs 0.251 ms).
 __device__ __forceinline__ f2v cmul_rt(f2v a, f2v w) {
   return f2v{__builtin_fmaf(-a.y, w.y, a.x * w.x), __builtin_fmaf(a.y, w.x, a.x * w.y)};
 }
 __device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
   return f2v{__builtin_fmaf(a.y, w.y, a.x * w.x), __builtin_fmaf(-a.y, w.x, a.x * w.y)};
 }
-#else
-__device__ __forceinline__ f2v cmul_rt(f2v a, f2v w) {
-  f2v t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
-      : "=v"(r) : "v"(a), "v"(w), "v"(t));
-  return r;
-}
-__device__ __forceinline__ f2v cmul_conj_rt(f2v a, f2v w) {  // conj(a) * w
-  f2v t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
-      : "=v"(r) : "v"(a), "v"(w), "v"(t));
-  return r;
-}
-#endif
 // value the compiler must treat as defined without materialising it (skip paths of the
 // wave-uniform pass guards: otherwise the backend zero-fills every register of the butterfly)
 // An opaque unspecified value.  (freeze(poison) -- __builtin_nondeterministic_value -- removes the

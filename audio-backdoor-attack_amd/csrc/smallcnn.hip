@@ -207,12 +207,12 @@ __device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
 }
 
 // weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets), fc1^T
-constexpr int kGuardTickets = 4;  // BN1, BN2, BN3 guard tickets (+ a spare); the fc head's row tiles follow
+constexpr int kGuardTickets = 4;  // BN1, BN2, BN3 guard tickets (+ a spare)
 struct PrepArgs {
   const float *c2w, *c3w, *f1w;
   int flat;
   float *w2f, *w2d, *w3f, *w3d, *f1t;
-  unsigned* tickets;  // the step's arrival tickets (guards, head_fwd row tiles), zeroed here every step
+  unsigned* tickets;  // the step's guard arrival tickets, zeroed here every step
   int ntickets;
 };
 
@@ -527,7 +527,7 @@ struct GuardOut {
   BCoef* bcoef;
   unsigned* ticket;
 };
-// the last of n arrivals (n = gridDim.x for the guards, the split count for head_fwd's row tiles)
+// the last of n arrivals (n = gridDim.x)
 __device__ __forceinline__ bool last_arrival(unsigned* ticket, unsigned n) {
   __shared__ unsigned last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -549,7 +549,6 @@ __device__ __forceinline__ bool last_arrival(unsigned* ticket, unsigned n) {
   return last != 0u;
 }
 __device__ __forceinline__ bool guard_last_block(unsigned* ticket) { return last_arrival(ticket, gridDim.x); }
-__device__ __forceinline__ bool head_tile_last(unsigned* ticket, unsigned n) { return last_arrival(ticket, n); }
 __device__ __forceinline__ void guard_finalize(const float* part, int nblk, int C, const float* gamma, const GuardOut& g) {
   __shared__ double red[2][kT / kWave];
   for (int c = 0; c < C; ++c) {
@@ -3066,7 +3065,7 @@ struct Work {
   float* daT;              // fused fc head: da transposed (128 x B), head_dgrad's A operand
   uint16_t* p1s;           // conv2 plane mode: pool1 output m as exact bf16 planes [3][n_p1]
   uint16_t* dz2s;          // conv2 plane mode: BN2-backward output dz2 as planes [3][n_r2]
-  unsigned* tickets;       // guarded BN fallbacks' and head_fwd's arrival tickets (zeroed by the prep blocks)
+  unsigned* tickets;       // guarded BN fallbacks' arrival tickets (zeroed by the prep blocks)
   int ntickets;
   float* w2fold;           // BN1 fold (bn_finalize_kernel): conv2 forward weights times alpha
   double* ft2;             //   and the beta' bias terms [ci][co]
@@ -3201,7 +3200,7 @@ Work layout(const abd_cnn* net, int64_t B, char* base) {
   }
   w.p1s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_p1 * sizeof(uint16_t)));
   w.dz2s = reinterpret_cast<uint16_t*>(take((size_t)3 * n_r2 * sizeof(uint16_t)));
-  w.ntickets = kGuardTickets + (int)((B + 31) / 32);
+  w.ntickets = kGuardTickets;
   w.tickets = reinterpret_cast<unsigned*>(take((size_t)w.ntickets * sizeof(unsigned)));
   w.bytes = off;
   return w;
@@ -3318,11 +3317,10 @@ HeadArgs head_args(const abd_cnn* net, const Work& w, const Params& P, float* gr
   a.n_w1 = 4 * ((g.flat + 31) / 32);
   a.n_w2 = 4 * ((g.K + 31) / 32) + (g.K + 128 + kHeadW2 - 1) / kHeadW2;  // fc2 weight tiles + bias sums
   a.n_apply = head_napply(a.pool, B);
-  a.tickets = w.tickets + kGuardTickets;
   return a;
 }
 
-// launch 1 (forward: pool3 + dropout1 + fc1 partials, the row head in each tile's last block) / 2 (dp3 + BN3 sums) /
+// launch 1 (forward: pool3 + dropout1 + fc1 partials) / 2 (row head, then dp3 + BN3 sums) /
 // 3 (gradients + BN3 apply)
 int launch_head(int which, const HeadArgs& a, hipStream_t s) {
   if (which == 1) {
@@ -3335,6 +3333,10 @@ int launch_head(int which, const HeadArgs& a, hipStream_t s) {
     else head_fwd_kernel<8><<<grid, kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_FWD, s);
   } else if (which == 2) {
+    abd::prof_begin(abd::PH_HEAD_MID, s);
+    head_row_kernel<<<(unsigned)((a.B + kHeadRows - 1) / kHeadRows), kT, 0, s>>>(a);
+    abd::prof_end(abd::PH_HEAD_MID, s);
+    ABD_LAUNCH_CHECK();
     abd::prof_begin(abd::PH_HEAD_DGRAD, s);
     head_dgrad_kernel<<<dim3((unsigned)a.nft, (unsigned)a.nrb), kT, 0, s>>>(a);
     abd::prof_end(abd::PH_HEAD_DGRAD, s);
@@ -3619,11 +3621,12 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // K-step order (see the kernel): channel-group-major for the forward (conv2 0.147 -> 0.141 ms),
   // tap-major for the data gradient (0.133 vs 0.136 ms channel-major)
   const bool ko = EPI == EPI_CONV;
-  // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the data gradient
-  // measured slower through it (0.132 -> 0.141 ms: its tap masks and edge rows), so it stays on the
-  // direct kernel by default (ws_dma_mode)
+  // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the f32split data
+  // gradient measured no faster through it (r4_v4: 0.1309 direct vs 0.1316 staged), so it stays on
+  // the direct kernel by default (ws_dma_mode); bf16's plane-operand data gradient is staged
+  // (0.0702 -> 0.0683 ms)
   const int dma_mode = ws_dma_mode();
-  const bool dma = dma_mode == 2 || (dma_mode == 1 && EPI == EPI_CONV);
+  const bool dma = dma_mode == 2 || (dma_mode == 1 && (EPI == EPI_CONV || (PA && NP == 1)));
   // the forward's taps never leave the source grid; the data gradient's are masked in the kernel
   const bool fwd_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == 1 && a.dh[2] == 1 && a.dw[2] == 0 &&
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
