@@ -157,9 +157,12 @@ def test_train_step_gradients_vs_oracle(dev, shape, prec):
         assert nrel(sd[k].cpu().numpy(), o2.p[k]) < 1e-6, k
 
 
-def test_autograd_path_matches_oracle(dev):
-    """nn.Module forward + torch CrossEntropyLoss + .backward() (autograd Function over libabd)."""
-    H, W, K, B = 101, 40, 10, 32
+@pytest.mark.parametrize("B", [32, 1])
+def test_autograd_path_matches_oracle(dev, B):
+    """nn.Module forward + torch CrossEntropyLoss + .backward() (autograd Function over libabd).
+    B = 1: the DataLoader's 1-row tail (drop_last=False) -- BatchNorm2d normalises over N x H x W,
+    so one row is a valid train-mode batch on both paths."""
+    H, W, K = 101, 40, 10
     lf = oc.geometry(H, W)["flat"]
     st = make_state(H, W, K, lf, seed=77)
     m = build(st, K, lf, dev).train()
