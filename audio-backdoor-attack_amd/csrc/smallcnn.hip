@@ -2340,6 +2340,241 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
   }
 }
 
+// Weight-stationary conv2 GEMM in f32split with the A operand staged PRE-SPLIT (round 4).
+// conv_ws_dma_kernel<EPI, 3> splits every (row, tap) fragment of a 16-channel group after reading it
+// from its fp32 stage -- 32 rows x 4 taps of splits for ~48 distinct positions, 2.7x redundant --
+// and its LDS-DMA pieces cost 60-185 issue cycles each beside MFMAs (MI355X_MICROARCH.md); with the
+// split's VALU they crowd the issue slots the MFMAs need (forward ablation: no DMA issue 0.131 ->
+// 0.083 ms, no split -> 0.106).  Here each wave loads the group's span with plain buffer loads one
+// group ahead (units of 8 channels x 1 position, 32 B, <= 2 per lane), splits each unit ONCE into the
+// three exact bf16 planes, writes them to its own LDS stage (kPreRow = 56 bf16 = 112 B per position:
+// 3 planes x 32 B + 16 B pad, 7 bank groups apart, so 16 consecutive positions hit 16 distinct
+// groups), and the taps read the planes straight into the MFMA operands (3 ds_read_b128 per tap).
+// Same tiles, K order, products, summation order and epilogue as conv_ws_dma_kernel<EPI, 3>.
+// LDS: 101,376 (weights) + 57,344 (stages) + 4,352 = 163,072 B of the CU's 163,840.
+constexpr int kPreRow = 56;
+#ifndef ABD_WS_PRE  // measurement builds: 0 conv_ws_dma_kernel<EPI, 3> everywhere, 1 the conv2 forward,
+#define ABD_WS_PRE 3  // 2 + the conv2 data gradient (default ABD_WS_DMA=1 too), 3 + the conv3 forward
+#endif
+template <int EPI, int NJ = 2>
+__global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
+  constexpr int NP = 3, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 stage[WPB][kDmaSpan * kPreRow];
+  __shared__ float red[WPB][N][2];
+  __shared__ float bfold[N];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
+    const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    bf16x8 pl[NP];
+    planes_x8<NP>(lo, hi, pl);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
+  }
+  if (EPI == EPI_CONV && a.fold_t != nullptr) {
+    for (int q = tid; q < N * 8; q += WPB * 64) {
+      const int n = q / 8, part = q % 8;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < CS / 8; ++c) acc += a.fold_t[(int64_t)(part * (CS / 8) + c) * N + n];
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) bfold[n] = (float)(acc + (double)a.bias[n]);
+    }
+  }
+  __syncthreads();
+  const int64_t W = (int64_t)gridDim.x * WPB;
+  const int64_t g = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(wave);
+  const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
+  const int HoWo = a.Ho * a.Wo;
+  const int npos = a.Hs * a.Ws * (a.M / HoWo);
+  int tofs[4], tmin = 0, tmax = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    tofs[t] = a.dh[t] * a.Ws + a.dw[t];
+    tmin = min(tmin, tofs[t]);
+    tmax = max(tmax, tofs[t]);
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
+  const int kq = 8 * (lane >> 5);
+  float st[NJ][2];
+  float bias[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    st[j][0] = st[j][1] = 0.0f;
+    bias[j] = 0.0f;
+    if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
+  }
+  __bf16* sw = stage[__builtin_amdgcn_readfirstlane(wave)];
+  constexpr uint32_t kOOB = 0x80000000u;
+  // unit u = lane + 64 k: position u >> 1, channels cg * 16 + 8 (u & 1) .. + 7 of the group
+  auto fetch = [&](int p0, int cg, int need, float4 (&r)[2][2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = lane + 64 * k, pos = u >> 1;
+      const uint32_t off = pos < need ? (uint32_t)(((p0 + pos) * CS + cg * 16 + (u & 1) * 8) * 4) : kOOB;
+      r[k][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
+      r[k][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
+    }
+  };
+  auto put = [&](int need, const float4 (&r)[2][2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = lane + 64 * k, pos = u >> 1;
+      if (pos < need) {
+        bf16x8 pl[NP];
+        planes_x8<NP>(r[k][0], r[k][1], pl);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(sw + pos * kPreRow + q * 16 + (u & 1) * 8) = pl[q];
+      }
+    }
+  };
+  const int ntiles = (r_hi - r_lo + 31) / 32;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
+  auto src_of = [&](int m) {
+    const int b = m / HoWo, rem = m - b * HoWo;
+    const int h = rem / a.Wo, w = rem - h * a.Wo;
+    return (b * a.Hs + h) * a.Ws + w;
+  };
+  auto taps_of = [&](int m) {
+    const int b = m / HoWo, rem = m - b * HoWo;
+    const int h = rem / a.Wo, w = rem - h * a.Wo;
+    uint32_t mk = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int hs = h + a.dh[t], ws = w + a.dw[t];
+      if (hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
+    }
+    return mk;
+  };
+  auto span_base = [&](int m, int& need) {
+    const int s0 = src_of(min(m + (lane & 31), r_hi - 1));
+    int v = s0, u = s0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      v = min(v, __shfl_xor(v, o, 64));
+      u = max(u, __shfl_xor(u, o, 64));
+    }
+    const int base = __builtin_amdgcn_readfirstlane(v) + tmin;
+    need = __builtin_amdgcn_readfirstlane(u) + tmax + 1 - base;
+    return base;
+  };
+  bf16x8 bvs[2][NJ][NP];
+  auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
+    const int kb = t * CS + cg * 16 + kq;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
+  };
+  // Software pipeline over the wave's stream of groups (4 per tile): while group g's MFMAs run, its
+  // 12 A fragments are already in registers, group g + 1's planes are written to the stage (LDS
+  // executes a wave's DS instructions in order: g's reads precede the writes) and group g + 2's
+  // units are loading.
+  int need = kDmaSpan, needn = kDmaSpan;
+  int p0 = ntiles > 0 ? span_base(r_lo, need) : 0;
+  float4 raw[2][2];
+  fetch(p0, 0, ntiles > 0 ? need : 0, raw);
+  put(ntiles > 0 ? need : 0, raw);
+  fetch(p0, 1, ntiles > 0 ? need : 0, raw);
+  load_b(0, 0, bvs[0]);
+#pragma unroll 1
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int m0 = r_lo + 32 * tile;
+    const int mr = min(m0 + (lane & 31), r_hi - 1);
+    const int prow = src_of(mr) - p0;
+    const uint32_t tm = taps_of(mr);
+    const bool more = tile + 1 < ntiles;
+    const int p0n = span_base(more ? m0 + 32 : m0, needn);
+    const int nn = more ? needn : 0;  // staged positions of the next tile (0: nothing to stage)
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+#pragma unroll
+    for (int cg = 0; cg < G; ++cg) {
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 av[4][NP];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);  // an invalid tap's position is clamped
+        const __bf16* rp = sw + pos * kPreRow + kq;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) av[t][q] = *reinterpret_cast<const bf16x8*>(rp + q * 16);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // group g + 1 into the stage (this tile's next group, or the next tile's group 0)
+      put(cg + 1 < G ? need : nn, raw);
+      __builtin_amdgcn_sched_barrier(0);
+      // group g + 2's loads
+      if (cg + 2 < G) fetch(p0, cg + 2, need, raw);
+      else fetch(p0n, cg + 2 - G, nn, raw);
+      __builtin_amdgcn_sched_barrier(0);  // one group's loads live at a time (hoisted, they spill)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if constexpr (EPI != EPI_CONV) {  // data-gradient taps leave the source grid at its edges
+          if (!((tm >> t) & 1u)) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) av[t][q] = bf16x8{};
+          }
+        }
+        const int s = cg * 4 + t;
+        load_b(((s + 1) % (4 * G)) / 4, (s + 1) % 4, bvs[(s + 1) & 1]);
+        bf16x8 (&bv)[NJ][NP] = bvs[s & 1];
+#pragma unroll
+        for (int term = 0; term < Terms<NP>::n; ++term)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t][Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
+      }
+    }
+    p0 = p0n;
+    need = needn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const bool ok = m < r_hi;
+      const uint32_t ob = ok ? (uint32_t)((m - r_lo) * N + (lane & 31)) * 4u : kOOB;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float v = acc[j][r];
+        if constexpr (EPI == EPI_CONV) {
+          v = fmaxf(v + bias[j], 0.0f);
+          const float vs = ok ? v : 0.0f;
+          st[j][0] += vs;
+          st[j][1] = fmaf(vs, vs, st[j][1]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
+      }
+    }
+  }
+  if (EPI != EPI_CONV || a.part == nullptr) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+    const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+    if (lane < 32) {
+      red[wave][32 * j + lane][0] = s0;
+      red[wave][32 * j + lane][1] = s1;
+    }
+  }
+  __syncthreads();
+  if (tid < N) {
+    float s0 = 0.0f, s1 = 0.0f;
+    for (int w = 0; w < WPB; ++w) {
+      s0 += red[w][tid][0];
+      s1 += red[w][tid][1];
+    }
+    a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
+    a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
+  }
+}
+
 struct TNArgs {
   const float* D;
   int ldd;
@@ -3654,7 +3889,8 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // the direct kernel by default (ws_dma_mode); bf16's plane-operand data gradient is staged
   // (0.0702 -> 0.0683 ms)
   const int dma_mode = ws_dma_mode();
-  const bool dma = dma_mode == 2 || (dma_mode == 1 && (EPI == EPI_CONV || (PA && NP == 1)));
+  const bool dma = dma_mode == 2 || (dma_mode == 1 && (EPI == EPI_CONV || (PA && NP == 1) ||
+                                                      (ABD_WS_PRE >= 2 && NP == 3 && !PA && a.N == 64)));
   // the forward's taps never leave the source grid; the data gradient's are masked in the kernel
   const bool fwd_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == 1 && a.dh[2] == 1 && a.dw[2] == 0 &&
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
@@ -3665,6 +3901,8 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
     if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 64 && ABD_WS_PRE) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_dma_kernel<EPI, NP, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
