@@ -151,8 +151,11 @@ def cpu_threads():
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
 
 
-def cpu_baseline(batch, threads, n_train=4096, n_test=1024, warmup_steps=2):
-    """The reference CPU path on the bench's workload, as a bounded sample: torch-fp32
+def cpu_baseline(batch, threads, n_train=4096, n_test=1024, warmup_steps=5):
+    """The reference CPU path on the bench's workload (5 warmup steps, one timed
+    epoch, clean accuracy / ASR after it), as a bounded sample -- 4,096 of BASELINE's 20,480 training
+    clips, so the default bench finishes in minutes (the task's 10-30 s CPU budget) -- on the box's
+    CPU share (OMP_NUM_THREADS, 16; `affinity_cpus` reports sched_getaffinity, the whole host): torch-fp32
     restatement (oracle/torch_ref.py: torch.stft MFCC with torchaudio's semantics + nn smallcnn of the
     reference structure + torch Adam), ultrasonic K = 35, 10 % of the training clips poisoned.  After
     `warmup_steps` untimed steps, ONE full epoch over n_train clips at the bench batch is timed (per
