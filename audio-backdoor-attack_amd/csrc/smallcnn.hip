@@ -2351,8 +2351,16 @@ __global__ void __launch_bounds__(512, 1) conv_ws_dma_kernel(NTArgs a) {
 // 3 planes x 32 B + 16 B pad, 7 bank groups apart, so 16 consecutive positions hit 16 distinct
 // groups), and the taps read the planes straight into the MFMA operands (3 ds_read_b128 per tap).
 // Same tiles, K order, products, summation order and epilogue as conv_ws_dma_kernel<EPI, 3>.
-// LDS: 101,376 (weights) + 57,344 (stages) + 4,352 = 163,072 B of the CU's 163,840.
+// LDS: 101,376 (weights) + 57,344 (stages; the data gradient's 58,240 with a zero position per
+// wave) + 256 = 158,976 / 159,872 B of the CU's 163,840 (the statistics' per-wave partials reuse
+// each wave's stage after its last tile).
+// Ablations (-DABD_PRE_ABL, results discarded; forward / data gradient, ms): 0.121 / 0.123 base; no
+// stage writes 0.099 / 0.093; no split 0.103 / 0.100; no loads 0.112 / 0.114; no output stores
+// 0.117 / 0.110; no MFMAs 0.093 / 0.088 -- the MFMAs are not what bounds it.
 constexpr int kPreRow = 56;
+#ifndef ABD_PRE_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads, 4 no MFMAs,
+#define ABD_PRE_ABL 0  // 8 no output stores, 16 no split (raw bits written to the planes)
+#endif
 #ifndef ABD_WS_PRE  // measurement builds: 0 conv_ws_dma_kernel<EPI, 3> everywhere, 1 the conv2 forward,
 #define ABD_WS_PRE 3  // 2 + the conv2 data gradient (default ABD_WS_DMA=1 too), 3 + the conv3 forward
 #endif
@@ -2360,8 +2368,14 @@ template <int EPI, int NJ = 2>
 __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
   constexpr int NP = 3, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, G = CS / 16;
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
-  __shared__ __attribute__((aligned(16))) __bf16 stage[WPB][kDmaSpan * kPreRow];
-  __shared__ float red[WPB][N][2];
+  // data gradient: an out-of-grid tap reads the stage's zero position (one address select per tap
+  // instead of zeroing its 12 fragment registers; dgrad -3 us)
+  constexpr bool ZROW = EPI != EPI_CONV;
+  constexpr int SPOS = kDmaSpan + (ZROW ? 1 : 0);  // staged positions per wave (+ the zero position)
+  __shared__ __attribute__((aligned(16))) __bf16 stage[WPB][SPOS * kPreRow];
+  // the statistics' per-wave partials reuse the wave's own stage once its tiles are done
+  static_assert(N * 2 * sizeof(float) <= SPOS * kPreRow * sizeof(__bf16), "red fits a stage");
+  auto red = [&](int w) { return reinterpret_cast<float (*)[2]>(&stage[w][0]); };
   __shared__ float bfold[N];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
@@ -2409,6 +2423,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
     if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
   }
   __bf16* sw = stage[__builtin_amdgcn_readfirstlane(wave)];
+  if constexpr (ZROW) {
+    if (lane < kPreRow / 8) *reinterpret_cast<bf16x8*>(sw + kDmaSpan * kPreRow + lane * 8) = bf16x8{};
+  }
   constexpr uint32_t kOOB = 0x80000000u;
   // unit u = lane + 64 k: position u >> 1, channels cg * 16 + 8 (u & 1) .. + 7 of the group
   auto fetch = [&](int p0, int cg, int need, float4 (&r)[2][2]) {
@@ -2416,17 +2433,37 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
     for (int k = 0; k < 2; ++k) {
       const int u = lane + 64 * k, pos = u >> 1;
       const uint32_t off = pos < need ? (uint32_t)(((p0 + pos) * CS + cg * 16 + (u & 1) * 8) * 4) : kOOB;
+      if constexpr ((ABD_PRE_ABL & 2) != 0) {
+        typedef float fv4 __attribute__((ext_vector_type(4)));
+        fv4 z;
+        asm volatile("; abl" : "=v"(z) : "v"(off));
+        r[k][0] = r[k][1] = __builtin_bit_cast(float4, z);
+        continue;
+      }
       r[k][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
       r[k][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
     }
   };
   auto put = [&](int need, const float4 (&r)[2][2]) {
+    if constexpr ((ABD_PRE_ABL & 1) != 0) {
+      typedef float fv4 __attribute__((ext_vector_type(4)));
+      const fv4 x0 = __builtin_bit_cast(fv4, r[0][0]), x1 = __builtin_bit_cast(fv4, r[0][1]);
+      const fv4 x2 = __builtin_bit_cast(fv4, r[1][0]), x3 = __builtin_bit_cast(fv4, r[1][1]);
+      asm volatile("; abl" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(need));
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int u = lane + 64 * k, pos = u >> 1;
       if (pos < need) {
         bf16x8 pl[NP];
-        planes_x8<NP>(r[k][0], r[k][1], pl);
+        if constexpr ((ABD_PRE_ABL & 16) != 0) {
+          pl[0] = __builtin_bit_cast(bf16x8, r[k][0]);
+          pl[1] = __builtin_bit_cast(bf16x8, r[k][1]);
+          pl[2] = pl[0];
+        } else {
+          planes_x8<NP>(r[k][0], r[k][1], pl);
+        }
 #pragma unroll
         for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(sw + pos * kPreRow + q * 16 + (u & 1) * 8) = pl[q];
       }
@@ -2483,7 +2520,10 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
     need = __builtin_amdgcn_readfirstlane(u) + tmax + 1 - base;
     return base;
   };
-  bf16x8 bvs[2][NJ][NP];
+  // B fragments are loaded BD steps ahead (NBV buffers, a power of two: the 16 steps of a tile keep
+  // the buffer order across tiles); 2 steps ahead: forward -2, data gradient -1.5 us against 1
+  constexpr int BD = 2, NBV = 4;
+  bf16x8 bvs[NBV][NJ][NP];
   auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
     const int kb = t * CS + cg * 16 + kq;
 #pragma unroll
@@ -2501,7 +2541,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
   fetch(p0, 0, ntiles > 0 ? need : 0, raw);
   put(ntiles > 0 ? need : 0, raw);
   fetch(p0, 1, ntiles > 0 ? need : 0, raw);
-  load_b(0, 0, bvs[0]);
+#pragma unroll
+  for (int s = 0; s < BD; ++s) load_b(s / 4, s % 4, bvs[s]);
 #pragma unroll 1
   for (int tile = 0; tile < ntiles; ++tile) {
     const int m0 = r_lo + 32 * tile;
@@ -2523,7 +2564,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
       bf16x8 av[4][NP];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);  // an invalid tap's position is clamped
+        int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);  // an invalid tap's position is clamped
+        if constexpr (ZROW) pos = (tm >> t) & 1u ? pos : kDmaSpan;  // ... or the zero position
         const __bf16* rp = sw + pos * kPreRow + kq;
 #pragma unroll
         for (int q = 0; q < NP; ++q) av[t][q] = *reinterpret_cast<const bf16x8*>(rp + q * 16);
@@ -2538,20 +2580,25 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
       __builtin_amdgcn_sched_barrier(0);  // one group's loads live at a time (hoisted, they spill)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        if constexpr (EPI != EPI_CONV) {  // data-gradient taps leave the source grid at its edges
+        if constexpr (EPI != EPI_CONV && !ZROW) {  // data-gradient taps leave the source grid at its edges
           if (!((tm >> t) & 1u)) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) av[t][q] = bf16x8{};
           }
         }
         const int s = cg * 4 + t;
-        load_b(((s + 1) % (4 * G)) / 4, (s + 1) % 4, bvs[(s + 1) & 1]);
-        bf16x8 (&bv)[NJ][NP] = bvs[s & 1];
+        load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
+        bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
 #pragma unroll
         for (int term = 0; term < Terms<NP>::n; ++term)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j)
+          for (int j = 0; j < NJ; ++j) {
+            if constexpr ((ABD_PRE_ABL & 4) != 0) {
+              asm volatile("; abl" ::"v"(av[t][Terms<NP>::A[term]]), "v"(bv[j][Terms<NP>::B[term]]));
+              continue;
+            }
             acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t][Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
+          }
       }
     }
     p0 = p0n;
@@ -2573,6 +2620,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
           st[j][0] += vs;
           st[j][1] = fmaf(vs, vs, st[j][1]);
         }
+        if ((ABD_PRE_ABL & 8) && __builtin_bit_cast(uint32_t, v) != 0x7fc00001u) continue;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
       }
     }
@@ -2583,16 +2631,16 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
     const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
     const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
     if (lane < 32) {
-      red[wave][32 * j + lane][0] = s0;
-      red[wave][32 * j + lane][1] = s1;
+      red(wave)[32 * j + lane][0] = s0;
+      red(wave)[32 * j + lane][1] = s1;
     }
   }
   __syncthreads();
   if (tid < N) {
     float s0 = 0.0f, s1 = 0.0f;
     for (int w = 0; w < WPB; ++w) {
-      s0 += red[w][tid][0];
-      s1 += red[w][tid][1];
+      s0 += red(w)[tid][0];
+      s1 += red(w)[tid][1];
     }
     a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
     a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
