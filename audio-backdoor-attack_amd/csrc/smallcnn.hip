@@ -2647,6 +2647,307 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
   }
 }
 
+// Weight-stationary conv GEMM in f32split with WAVE-SPECIALISED staging (round 4).  The ablations of
+// conv_ws_pre_kernel (no MFMAs: still 0.093 ms of 0.121) show its every-wave chain -- loads, split,
+// LDS writes, fragment reads, MFMAs -- bound by latency at 2 waves per SIMD, with the matrix pipe
+// ~45 % busy.  Here the two waves of a SIMD split the roles: waves 0-3 (one per SIMD) only read
+// fragments and run the MFMAs and the epilogue; waves 4-7 (their SIMD partners) load the consumer's
+// span two groups ahead, split each unit once into the three exact bf16 planes and write them into
+// the consumer's double-buffered stage, so the split's VALU co-executes with the partner's MFMAs.
+// One block barrier per 16-channel group publishes group q + 1 while the consumer reads group q.
+// Every wave runs the same number of groups (the longest consumer's; rows past r_hi are masked).
+// Same tiles (32 rows x 32 NJ columns per consumer tile), K order, products and epilogue as
+// conv_ws_pre_kernel, so results are identical to it.  LDS: 101,376 (weights) + 57,344 / 58,240
+// (4 consumers x 2 buffers x 64 positions x 112 B, + a zero position per buffer in the data
+// gradient) + 256 B.
+#ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
+#define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
+#endif
+#ifndef ABD_WS_SPEC  // 1: conv_ws_spec_kernel replaces conv_ws_pre_kernel (measurement builds: 0)
+#define ABD_WS_SPEC 1
+#endif
+template <int EPI, int NJ = 2>
+__global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
+  constexpr int NP = 3, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, NC = 4, G = CS / 16;
+  static_assert(G == 4, "the group parity selects the stage buffer; the producer loads one tile ahead");
+  constexpr bool ZROW = EPI != EPI_CONV;
+  constexpr int SPOS = kDmaSpan + (ZROW ? 1 : 0);
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP][N * LD];
+  __shared__ __attribute__((aligned(16))) __bf16 stage[NC][2][SPOS * kPreRow];
+  __shared__ float bfold[N];
+  static_assert(N * 2 * sizeof(float) <= SPOS * kPreRow * sizeof(__bf16), "red fits a stage buffer");
+  auto red = [&](int w) { return reinterpret_cast<float (*)[2]>(&stage[w][0][0]); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < N * (K / 8); idx += WPB * 64) {
+    const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8);
+    const float4 hi = *reinterpret_cast<const float4*>(a.Bw + (int64_t)n * a.ldb + k8 + 4);
+    bf16x8 pl[NP];
+    planes_x8<NP>(lo, hi, pl);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(&Bs[q][n * LD + k8]) = pl[q];
+  }
+  if (EPI == EPI_CONV && a.fold_t != nullptr) {
+    for (int q = tid; q < N * 8; q += WPB * 64) {
+      const int n = q / 8, part = q % 8;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < CS / 8; ++c) acc += a.fold_t[(int64_t)(part * (CS / 8) + c) * N + n];
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) bfold[n] = (float)(acc + (double)a.bias[n]);
+    }
+  }
+  const bool producer = __builtin_amdgcn_readfirstlane(wave) >= NC;
+  const int c = __builtin_amdgcn_readfirstlane(wave) & (NC - 1);  // the consumer this wave is or serves
+  if constexpr (ZROW) {
+    if (!producer && lane < 2 * (kPreRow / 8))
+      *reinterpret_cast<bf16x8*>(&stage[c][lane / (kPreRow / 8)][kDmaSpan * kPreRow + (lane % (kPreRow / 8)) * 8]) = bf16x8{};
+  }
+  const int64_t W = (int64_t)gridDim.x * NC;
+  const int64_t g = (int64_t)blockIdx.x * NC + c;
+  const int r_lo = (int)(a.M * g / W), r_hi = (int)(a.M * (g + 1) / W);
+  const int nt = (int)((a.M + W - 1) / W + 31) / 32;  // tiles of every wave (the longest consumer's)
+  const int HoWo = a.Ho * a.Wo;
+  const int npos = a.Hs * a.Ws * (a.M / HoWo);
+  int tofs[4], tmin = 0, tmax = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    tofs[t] = a.dh[t] * a.Ws + a.dw[t];
+    tmin = min(tmin, tofs[t]);
+    tmax = max(tmax, tofs[t]);
+  }
+  constexpr uint32_t kOOB = 0x80000000u;
+  // this wave's (consumer's) output row of the current tile, stepped 32 rows per tile as in
+  // conv_ws_pre_kernel (rows past r_hi continue the pattern; past the last image they load zeros)
+  const int dH = 32 / a.Wo, dW = 32 - dH * a.Wo;
+  int cb, ch, cw;
+  {
+    const int m = r_lo + (lane & 31);
+    cb = m / HoWo;
+    const int rem = m - cb * HoWo;
+    ch = rem / a.Wo;
+    cw = rem - ch * a.Wo;
+  }
+  auto step32 = [&](int& b, int& h, int& w) {
+    w += dW;
+    h += dH;
+    if (w >= a.Wo) {
+      w -= a.Wo;
+      ++h;
+    }
+    while (h >= a.Ho) {
+      h -= a.Ho;
+      ++b;
+    }
+  };
+  auto src_at = [&](int b, int h, int w) { return (b * a.Hs + h) * a.Ws + w; };
+  auto span_of = [&](int s0, int& need) {
+    int v = s0, u = s0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      v = min(v, __shfl_xor(v, o, 64));
+      u = max(u, __shfl_xor(u, o, 64));
+    }
+    const int base = __builtin_amdgcn_readfirstlane(v) + tmin;
+    need = __builtin_amdgcn_readfirstlane(u) + tmax + 1 - base;
+    return base;
+  };
+  if (producer) {
+    // ---- producer: group q + 1 into buffer (q + 1) & 1 while the consumer reads group q ----
+    const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
+    auto fetch = [&](int p0, int cg, int need, float4 (&r)[2][2]) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pos = (lane & 31) + 32 * k, h = lane >> 5;
+        const uint32_t off = pos < need ? (uint32_t)(((p0 + pos) * CS + cg * 16 + h * 8) * 4) : kOOB;
+        if constexpr ((ABD_SPEC_ABL & 2) != 0) {
+          typedef float fv4 __attribute__((ext_vector_type(4)));
+          fv4 z;
+          asm volatile("; abl" : "=v"(z) : "v"(off));
+          r[k][0] = r[k][1] = __builtin_bit_cast(float4, z);
+          continue;
+        }
+        r[k][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
+        r[k][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)(off + 16u), 0, 0));
+      }
+    };
+    // every position of the span buffer is written (past `need` the loads returned zeros).  Unit
+    // (lane, k) = channels 8 (lane >> 5) .. + 7 of position (lane & 31) + 32 k: a ds_write_b128's
+    // 8-lane bank group then writes 8 consecutive positions 112 B apart, distinct banks (the
+    // position-pair order of conv_ws_pre_kernel 2-way conflicts), and a load still touches 32 lines
+    auto put = [&](__bf16* sw, const float4 (&r)[2][2]) {
+      if constexpr ((ABD_SPEC_ABL & 1) != 0) {
+        typedef float fv4 __attribute__((ext_vector_type(4)));
+        const fv4 x0 = __builtin_bit_cast(fv4, r[0][0]), x1 = __builtin_bit_cast(fv4, r[0][1]);
+        const fv4 x2 = __builtin_bit_cast(fv4, r[1][0]), x3 = __builtin_bit_cast(fv4, r[1][1]);
+        asm volatile("; abl" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(sw));
+        return;
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pos = (lane & 31) + 32 * k, h = lane >> 5;
+        bf16x8 pl[NP];
+        planes_x8<NP>(r[k][0], r[k][1], pl);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x8*>(sw + pos * kPreRow + q * 16 + h * 8) = pl[q];
+      }
+    };
+    // loads run RB = 4 groups ahead of their put (one tile): group q + 1 is put from raw[(q + 1) % 4]
+    // and that buffer then loads group q + 5 (the next tile's cg + 1, or the tile after's group 0)
+    int need0 = 0, need1 = 0, need2 = 0;
+    const int p00 = span_of(src_at(cb, ch, cw), need0);  // tile 0
+    step32(cb, ch, cw);
+    int p01 = span_of(src_at(cb, ch, cw), need1);  // the tile after the one being put
+    step32(cb, ch, cw);
+    int p02 = span_of(src_at(cb, ch, cw), need2);  // the one after that
+    if (nt < 2) need1 = 0;
+    if (nt < 3) need2 = 0;
+    float4 raw[4][2][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) fetch(p00, q, need0, raw[q]);
+    __syncthreads();  // weights, bfold and the zero positions
+    put(stage[c][0], raw[0]);
+    fetch(p01, 0, need1, raw[0]);
+    __syncthreads();
+#pragma unroll 1
+    for (int tile = 0; tile < nt; ++tile) {
+#pragma unroll
+      for (int cg = 0; cg < G; ++cg) {
+        if (cg + 1 < G || tile + 1 < nt) put(stage[c][(cg + 1) & 1], raw[(cg + 1) % 4]);
+        if (cg + 1 < G) fetch(p01, cg + 1, need1, raw[(cg + 1) % 4]);
+        else fetch(p02, 0, need2, raw[0]);
+        __syncthreads();
+      }
+      p01 = p02;
+      need1 = need2;
+      step32(cb, ch, cw);
+      p02 = span_of(src_at(cb, ch, cw), need2);
+      if (tile + 3 >= nt) need2 = 0;
+    }
+  } else {
+    // ---- consumer: fragments of group q from buffer q & 1, MFMAs, epilogue per tile ----
+    const int kq = 8 * (lane >> 5);
+    float st[NJ][2];
+    float bias[NJ];
+    __syncthreads();  // weights, bfold and the zero positions
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      st[j][0] = st[j][1] = 0.0f;
+      bias[j] = 0.0f;
+      if constexpr (EPI == EPI_CONV) bias[j] = a.fold_t != nullptr ? bfold[32 * j + (lane & 31)] : a.bias[32 * j + (lane & 31)];
+    }
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (int64_t)r_lo * N, 0, (r_hi - r_lo) * N * 4, 0x00020000);
+    auto taps_at = [&](int h, int w) {
+      uint32_t mk = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int hs = h + a.dh[t], ws = w + a.dw[t];
+        if (hs >= 0 && hs < a.Hs && ws >= 0 && ws < a.Ws) mk |= 1u << t;
+      }
+      return mk;
+    };
+    constexpr int BD = 2, NBV = 4;  // B fragments two steps ahead (as conv_ws_pre_kernel)
+    bf16x8 bvs[NBV][NJ][NP];
+    auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
+      const int kb = t * CS + cg * 16 + kq;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
+    };
+#pragma unroll
+    for (int s = 0; s < BD; ++s) load_b(s / 4, s % 4, bvs[s]);
+    __syncthreads();  // group 0 staged
+#pragma unroll 1
+    for (int tile = 0; tile < nt; ++tile) {
+      const int m0 = r_lo + 32 * tile;
+      int need;
+      const int prow = src_at(cb, ch, cw) - span_of(src_at(cb, ch, cw), need);
+      const uint32_t tm = taps_at(ch, cw);
+      step32(cb, ch, cw);
+      f32x16 acc[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+#pragma unroll
+      for (int cg = 0; cg < G; ++cg) {
+        const __bf16* sw = stage[c][cg & 1];
+        bf16x8 av[4][NP];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);
+          if constexpr (ZROW) pos = (tm >> t) & 1u ? pos : kDmaSpan;
+          const __bf16* rp = sw + pos * kPreRow + kq;
+#pragma unroll
+          for (int q = 0; q < NP; ++q) av[t][q] = *reinterpret_cast<const bf16x8*>(rp + q * 16);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int s = cg * 4 + t;
+          load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
+          bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
+#pragma unroll
+          for (int term = 0; term < Terms<NP>::n; ++term)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              if constexpr ((ABD_SPEC_ABL & 4) != 0) {
+                asm volatile("; abl" ::"v"(av[t][Terms<NP>::A[term]]), "v"(bv[j][Terms<NP>::B[term]]));
+                continue;
+              }
+              acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t][Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
+            }
+        }
+        if (cg + 1 < G) __syncthreads();  // the last group's barrier follows the epilogue
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const bool ok = m < r_hi;
+        const uint32_t ob = ok ? (uint32_t)((m - r_lo) * N + (lane & 31)) * 4u : kOOB;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          float v = acc[j][r];
+          if constexpr (EPI == EPI_CONV) {
+            v = fmaxf(v + bias[j], 0.0f);
+            const float vs = ok ? v : 0.0f;
+            st[j][0] += vs;
+            st[j][1] = fmaf(vs, vs, st[j][1]);
+          }
+          if ((ABD_SPEC_ABL & 8) && __builtin_bit_cast(uint32_t, v) != 0x7fc00001u) continue;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+    if (EPI == EPI_CONV && a.part != nullptr) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float s0 = st[j][0] + __shfl_xor(st[j][0], 32, 64);
+        const float s1 = st[j][1] + __shfl_xor(st[j][1], 32, 64);
+        if (lane < 32) {
+          red(c)[32 * j + lane][0] = s0;
+          red(c)[32 * j + lane][1] = s1;
+        }
+      }
+    }
+  }
+  if (EPI != EPI_CONV || a.part == nullptr) return;
+  __syncthreads();
+  if (tid < N) {
+    float s0 = 0.0f, s1 = 0.0f;
+    for (int w = 0; w < NC; ++w) {
+      s0 += red(w)[tid][0];
+      s1 += red(w)[tid][1];
+    }
+    a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
+    a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
+  }
+}
+
 struct TNArgs {
   const float* D;
   int ldd;
@@ -3973,6 +4274,8 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
     if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 64 && ABD_WS_PRE && ABD_WS_SPEC) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3 && ABD_WS_SPEC) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (NP == 3 && a.N == 64 && ABD_WS_PRE) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
