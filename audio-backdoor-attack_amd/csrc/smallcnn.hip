@@ -2663,8 +2663,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
 #define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
 #endif
-#ifndef ABD_WS_SPEC  // 1: conv_ws_spec_kernel replaces conv_ws_pre_kernel (measurement builds: 0)
-#define ABD_WS_SPEC 1
+#ifndef ABD_WS_SPEC  // conv_ws_spec_kernel replaces conv_ws_pre_kernel: 2 everywhere, 1 the forwards
+#define ABD_WS_SPEC 2  // only, 0 nowhere (measurement builds)
 #endif
 template <int EPI, int NJ = 2>
 __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
@@ -2885,10 +2885,14 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
 #pragma unroll
           for (int q = 0; q < NP; ++q) av[t][q] = *reinterpret_cast<const bf16x8*>(rp + q * 16);
         }
+        // all 12 A reads issue here (left to itself the compiler sinks each read to its first use
+        // and waits on it there: with one MFMA wave per SIMD every LDS latency was exposed)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int s = cg * 4 + t;
           load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
+          __builtin_amdgcn_sched_barrier(0);
           bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
 #pragma unroll
           for (int term = 0; term < Terms<NP>::n; ++term)
@@ -4273,9 +4277,10 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // (PA, conv2) staged as bf16
   if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
+    constexpr bool spec = ABD_WS_SPEC >= 2 || (ABD_WS_SPEC == 1 && EPI == EPI_CONV);
     if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 64 && ABD_WS_PRE && ABD_WS_SPEC) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3 && ABD_WS_SPEC) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 64 && ABD_WS_PRE && spec) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3 && spec) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (NP == 3 && a.N == 64 && ABD_WS_PRE) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
