@@ -2663,6 +2663,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
 #define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
 #endif
+#ifndef ABD_SPEC_ILV  // consumer read schedule: 2 (default) A one tap ahead and every step's reads
+#define ABD_SPEC_ILV 2  // one per MFMA gap; 1 only B interleaved; 0 all 18 reads at the group start
+#endif                 // (A/B, 3 alternations: 1.0007 / 0.9916 / 0.9894 ms per step)
 #ifndef ABD_WS_SPEC  // conv_ws_spec_kernel replaces conv_ws_pre_kernel: 2 everywhere, 1 the forwards
 #define ABD_WS_SPEC 2  // only, 0 nowhere (measurement builds)
 #endif
@@ -2876,6 +2879,44 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
 #pragma unroll
       for (int cg = 0; cg < G; ++cg) {
         const __bf16* sw = stage[c][cg & 1];
+#if ABD_SPEC_ILV >= 2
+        // A fragments one tap ahead (two register sets), B two steps ahead; each step's reads go
+        // one per MFMA gap
+        bf16x8 avb[2][NP];
+        auto load_a = [&](int t, bf16x8 (&av)[NP]) {
+          int pos = min(max(prow + tofs[t], 0), kDmaSpan - 1);
+          if constexpr (ZROW) pos = (tm >> t) & 1u ? pos : kDmaSpan;
+          const __bf16* rp = sw + pos * kPreRow + kq;
+#pragma unroll
+          for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(rp + q * 16);
+        };
+        load_a(0, avb[0]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int s = cg * 4 + t;
+          load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
+          if (t + 1 < 4) load_a(t + 1, avb[(t + 1) & 1]);
+#pragma unroll
+          for (int x = 0; x < NJ * NP + (t + 1 < 4 ? NP : 0); ++x) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          if (t + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - NJ * NP - NP, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - NJ * NP, 0);
+          bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
+          bf16x8 (&av)[NP] = avb[t & 1];
+#pragma unroll
+          for (int term = 0; term < Terms<NP>::n; ++term)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              if constexpr ((ABD_SPEC_ABL & 4) != 0) {
+                asm volatile("; abl" ::"v"(av[Terms<NP>::A[term]]), "v"(bv[j][Terms<NP>::B[term]]));
+                continue;
+              }
+              acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
+            }
+        }
+#else
         bf16x8 av[4][NP];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -2892,7 +2933,17 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
         for (int t = 0; t < 4; ++t) {
           const int s = cg * 4 + t;
           load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
+#if ABD_SPEC_ILV
+          // the step's B reads one per MFMA gap instead of a burst (LDS issue stalls)
+#pragma unroll
+          for (int x = 0; x < NJ * NP; ++x) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - NJ * NP, 0);
+#else
           __builtin_amdgcn_sched_barrier(0);
+#endif
           bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
 #pragma unroll
           for (int term = 0; term < Terms<NP>::n; ++term)
@@ -2905,6 +2956,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
               acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t][Terms<NP>::A[term]], bv[j][Terms<NP>::B[term]], acc[j], 0, 0, 0);
             }
         }
+#endif
         if (cg + 1 < G) __syncthreads();  // the last group's barrier follows the epilogue
       }
 #pragma unroll
