@@ -3244,6 +3244,9 @@ typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
 //     LDS latency is off the MFMA path and the lgkmcnt range (15) still covers the older reads.
 // NS = Qd / 16 steps and MAXS staging slots are compile-time (checked by the launcher); slots
 // past the images write a trash row (row Qd + Qs of each buffer).
+#ifndef ABD_TRP_ILV  // measurement builds: the next step's fragment reads PER per MFMA gap (0: a burst)
+#define ABD_TRP_ILV 0
+#endif
 #ifndef ABD_TRP_ABL  // ablation bits (measurement builds): 1 no MFMAs, 2 no staging writes, 4 no loads
 #define ABD_TRP_ABL 0
 #endif
@@ -3404,7 +3407,24 @@ __global__ void __launch_bounds__(kT, 1) conv_wgrad_trp_kernel(WGArgs a) {
       // 1-5 also wait for most of the new reads
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       if (s + 1 < NS) load_frags(cur, s + 1, F[(s + 1) & 1]);
+#if ABD_TRP_ILV
+      if constexpr (NTERM > 1) {
+        // the next step's reads spread over this step's MFMA gaps instead of one burst
+        constexpr int MF = (NTERM - 1) * NT * 2, RD = (NT + 2) * NP * 2, PER = ABD_TRP_ILV;
+        constexpr int NG = (RD + PER - 1) / PER < MF ? (RD + PER - 1) / PER : MF;
+        if (s + 1 < NS) {
+#pragma unroll
+          for (int x = 0; x < NG; ++x) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, PER, 0);
+          }
+        }
+      } else {
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#else
       __builtin_amdgcn_sched_barrier(0);
+#endif
       if constexpr (NTERM == 1) {
 #pragma unroll
         for (int k = 0; k < MAXS; ++k)  // slot k rides on step k % NS
