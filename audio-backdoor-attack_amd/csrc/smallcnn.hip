@@ -3244,8 +3244,8 @@ typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
 //     LDS latency is off the MFMA path and the lgkmcnt range (15) still covers the older reads.
 // NS = Qd / 16 steps and MAXS staging slots are compile-time (checked by the launcher); slots
 // past the images write a trash row (row Qd + Qs of each buffer).
-#ifndef ABD_TRP_ILV  // measurement builds: the next step's fragment reads PER per MFMA gap (0: a burst)
-#define ABD_TRP_ILV 0
+#ifndef ABD_TRP_ILV  // the next step's fragment reads PER per MFMA gap (0: one burst after term 0);
+#define ABD_TRP_ILV 2  // conv2 weight gradient 0.109 -> 0.104 ms (A/B, 3 alternations; PER 1: 0.1045)
 #endif
 #ifndef ABD_TRP_ABL  // ablation bits (measurement builds): 1 no MFMAs, 2 no staging writes, 4 no loads
 #define ABD_TRP_ABL 0
