@@ -2663,9 +2663,10 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
 #define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
 #endif
-#ifndef ABD_SPEC_ILV  // consumer read schedule: 2 (default) A one tap ahead and every step's reads
-#define ABD_SPEC_ILV 2  // one per MFMA gap; 1 only B interleaved; 0 all 18 reads at the group start
-#endif                 // (A/B, 3 alternations: 1.0007 / 0.9916 / 0.9894 ms per step)
+#ifndef ABD_SPEC_ILV  // consumer read schedule: 3 (default) A one tap ahead and every step's reads
+#define ABD_SPEC_ILV 3  // two per MFMA gap; 2 one per gap; 1 only B interleaved; 0 all 18 reads at the
+#endif                 // group start (A/B, 3 alternations: 0 1.0007, 1 0.9916, 2 0.9894 ms per step;
+                       // 2 vs 3 on another box: forward 0.1179 vs 0.1164, data gradient 0.1223 vs 0.1207)
 #ifndef ABD_WS_SPEC  // conv_ws_spec_kernel replaces conv_ws_pre_kernel: 2 everywhere, 1 the forwards
 #define ABD_WS_SPEC 2  // only, 0 nowhere (measurement builds)
 #endif
@@ -2896,13 +2897,23 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
           const int s = cg * 4 + t;
           load_b(((s + BD) % (4 * G)) / 4, (s + BD) % 4, bvs[(s + BD) % NBV]);
           if (t + 1 < 4) load_a(t + 1, avb[(t + 1) & 1]);
+          constexpr int PER = ABD_SPEC_ILV >= 3 ? 2 : 1;  // reads per MFMA gap
+          constexpr int G1 = (NJ * NP + NP + PER - 1) / PER, G0 = (NJ * NP + PER - 1) / PER;
+          if (t + 1 < 4) {
 #pragma unroll
-          for (int x = 0; x < NJ * NP + (t + 1 < 4 ? NP : 0); ++x) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            for (int x = 0; x < G1; ++x) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, PER, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - G1, 0);
+          } else {
+#pragma unroll
+            for (int x = 0; x < G0; ++x) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, PER, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - G0, 0);
           }
-          if (t + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - NJ * NP - NP, 0);
-          else __builtin_amdgcn_sched_group_barrier(0x008, Terms<NP>::n * NJ - NJ * NP, 0);
           bf16x8 (&bv)[NJ][NP] = bvs[s % NBV];
           bf16x8 (&av)[NP] = avb[t & 1];
 #pragma unroll
