@@ -52,6 +52,7 @@ constexpr bool kGatherV4 = true;
 
 struct MfccDev {
   int N, hop, pad, pad_mode, M, bluestein, n_freqs, n_mels, n_mfcc, T, ppb, chunks, n_pass, fast;
+  int dct_lds;  // db_dct_lds_kernel allowed (every plan but ABD_GENERIC_FFT's, when dct_tiles == 0)
   int ablate;  // diagnostics only (0 in the library; measurement builds set it): 1 skip sample loads, 2 skip FFTs, 4 skip mel
   int64_t L;
   float top_db;
@@ -660,9 +661,10 @@ template <int N>
 __device__ constexpr TwTab<N> kTw{};
 
 // ---- butterflies on ext_vector_type(2) complex values.  Every multiplication by -i / +i is
-// written as fma(swap(d), {1,-1}, t) (exact: *1 and *-1 are exact), which the backend emits as
-// one v_pk_fma_f32 with op_sel/neg modifiers; the struct float2 versions above compile to
-// packed adds plus v_mov pairs that re-assemble halves (~27 % of the FFT's VALU).
+// written as fma(swap(d), {1,-1}, t) (exact: *1 and *-1 are exact).  With packed FP32 the backend
+// emitted one v_pk_fma_f32 with op_sel/neg modifiers; this library is built without packed FP32
+// (Makefile PKFLAGS: op_sel-swapped v_pk_* low lanes go wrong under GPU sharing),
+// so each is two v_fma_f32 / v_sub_f32 on the halves.
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v vswap(f2v a) { return __builtin_shufflevector(a, a, 1, 0); }
 __device__ __forceinline__ f2v fmav(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
@@ -1336,8 +1338,8 @@ constexpr int kBlueBlocks = 8;
 //          per bin into a contiguous array placed past the FFT outputs that are still read
 //          (Z[k], k < N), so the reads and writes need no barrier between them;
 //   mel:   thread = half-filter slot (2 m + h, 2 n_mels == kThreads), kMelHP zero-padded weights
-//          per slot (p.mel3_w), every read base + immediate, one v_pk_fma per bin for both
-//          frames; the halves are combined by a lane swap, lane h writes frame 2 p0 + h.
+//          per slot (p.mel3_w), every read base + immediate, one float2 FMA per bin for both
+//          frames (two v_fma_f32 in the scalar build); the halves are combined by a lane swap, lane h writes frame 2 p0 + h.
 constexpr int kMelHP = 16;  // padded bins per half-filter slot of the Bluestein fast path
 template <int M, int NN>
 __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const MfccDev& p, float* __restrict__ db_u,
@@ -2265,6 +2267,7 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     }
   // B fragments of db_dct_mfma_kernel: [s][q][tile][col] -> float4 over j of dct[16 s + 4 q + j][16 tile + col]
   d.dct_tiles = (n_mels % 16 == 0 && n_mfcc <= 48 && !generic) ? (n_mfcc + 15) / 16 : 0;
+  d.dct_lds = generic ? 0 : 1;
   std::vector<float4> dfrag;
   if (d.dct_tiles > 0)
     for (int sg = 0; sg < n_mels / 16; ++sg)
@@ -2490,7 +2493,7 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
     else if (d.dct_tiles == 2) db_dct_mfma_kernel<2><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
     else db_dct_mfma_kernel<3><<<g, dim3(kThreads), 0, s>>>(d, ws_db, ws_max, ij, out);
   } else if (d.n_mfcc % 4 == 0 && dct_lds <= 64 * 1024 &&
-      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && d.fast) {
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && d.dct_lds) {
     db_dct_lds_kernel<<<dim3((unsigned)batch, (unsigned)((d.T + kTT2 - 1) / kTT2)), dim3(kThreads), dct_lds, s>>>(
         d, ws_db, ws_max, ij, out);
   } else {

@@ -190,7 +190,8 @@ __device__ __forceinline__ float bn_dx(float dy, float r, float4 /*cf*/, const B
 // parts' sum is the double to ~2^-48), dx = (B_hi r + g_hi dy + A_hi) + (B_lo r + g_lo dy + A_lo).
 // The batch-mean terms keep their double precision (no systematic bias for the cancelling
 // weight-gradient sums); what remains is the per-element fp32 rounding the double path also has
-// at its final store.  Channel pairs on v_pk_fma_f32 (conv1_wgrad_kernel); ABD_C1_DD=1 builds the
+// at its final store.  Channel pairs as float2 vector FMAs (conv1_wgrad_kernel; the library is built
+// without packed FP32, Makefile PKFLAGS, so each is two v_fma_f32); ABD_C1_DD=1 builds the
 // double-precision evaluation instead.
 struct BCoefF {
   float gh, gl, Ah, Al, Bh, Bl;
@@ -305,9 +306,9 @@ __device__ __forceinline__ C1W c1_weights(const C1Args& a, int c0) {
   return r;
 }
 
-// relu(conv1) at (hl, w) for 4 channels; same fma order as the oracle replay (b, w00, w01, w10, w11)
-// relu(conv1) for 4 channels at one position: channel pairs on v_pk_fma_f32, the same fma chain
-// per channel as the oracle replay (b, w00, w01, w10, w11)
+// relu(conv1) for 4 channels at one position: channel pairs as float2 vector FMAs (two v_fma_f32 each:
+// no packed FP32 in this library, Makefile PKFLAGS), the same fma chain per channel as the oracle
+// replay (b, w00, w01, w10, w11)
 typedef float c1f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ c1f2 c1_lo(const float4& v) { return c1f2{v.x, v.y}; }
 __device__ __forceinline__ c1f2 c1_hi(const float4& v) { return c1f2{v.z, v.w}; }
@@ -715,7 +716,7 @@ __global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
         xv[1][j] = (j <= nw) ? x0[a.g.W0 + j] : 0.0f;
       }
       const float dd[CPT] = {dvs[u].x, dvs[u].y};
-      // the channel pair on v_pk_fma_f32: per channel the same fma chain as the oracle replay
+      // the channel pair as float2 vector FMAs: per channel the same fma chain as the oracle replay
       // (b, w00, w01, w10, w11) and the same accumulation order
       float r[CPT][3];
   #pragma unroll
@@ -3211,7 +3212,8 @@ __global__ void __launch_bounds__(kT, 4) conv_wgrad_rows_kernel(WGArgs a) {
 // sum slabs in order; conv layout maps (n=co, k=t*Cin+ci) -> torch (co, ci, kh, kw)
 // Exact three-way bf16 split of 8 fp32 values (x = p0 + p1 + p2, see gemm_nt_bf16_kernel).
 __device__ __forceinline__ void split3_x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-  // pairs: v_cvt_pk_bf16_f32 (RNE), widen by bit moves, v_pk_add_f32 for the exact residual
+  // pairs: v_cvt_pk_bf16_f32 (RNE), widen by bit moves, a float2 subtraction for the exact residual
+  // (two v_sub_f32: no packed FP32 in this library, Makefile PKFLAGS)
   uint32_t u[3][4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {

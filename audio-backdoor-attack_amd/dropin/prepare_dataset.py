@@ -7,27 +7,18 @@ import os
 
 import numpy as np
 import torch
-from torch.utils.data import Dataset
 
 import _root  # noqa: F401
+from abd_amd import resident as _resident
 from abd_amd.features import MFCC, resample  # noqa: F401  (prepare_dataset.py:35-47, :60)
 from abd_amd.io import read_wav, LABEL_SETS, train_test_split_35
 
 __all__ = ["MFCC", "BDDataset", "prepare_clean_dataset", "load_clean_data"]
 
 
-class BDDataset(Dataset):
-    """Dict samples {'mfcc', 'label', 'poison_indicator'} (prepare_dataset.py:13-33)."""
-
-    def __init__(self, mfcc_list, label_list, poison_index):
-        self.mfcc_list, self.label_list, self.poison_index = mfcc_list, label_list, poison_index
-
-    def __len__(self):
-        return len(self.mfcc_list)
-
-    def __getitem__(self, index):
-        return {"mfcc": self.mfcc_list[index], "label": self.label_list[index],
-                "poison_indicator": self.poison_index[index]}
+class BDDataset(_resident.BDDataset):
+    """Dict samples {'mfcc', 'label', 'poison_indicator'} (prepare_dataset.py:13-33).  Loaders over it
+    feed training.train() / test() from HBM-resident copies (abd_amd/resident.py)."""
 
 
 def prepare_clean_dataset(data_path, directory_name, labels, waveform_to_consider, n_mfcc, n_fft, hop_length,

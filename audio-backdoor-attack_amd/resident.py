@@ -1,0 +1,163 @@
+"""HBM-resident DataLoader batches for the unchanged attack scripts' train() / test() loops.
+
+The scripts build ``DataLoader(BDDataset(...) | TensorDataset(...), batch_size, shuffle=True)``
+themselves (badnets.py:100-108, daba.py:149-154, flowmur.py:90-112) and the reference's train()
+walks it per batch (utils/training_tools.py:59-65): every batch is collated sample by sample on
+the host (``default_collate`` over dicts of tensor rows, prepare_dataset.py:22-31) and copied from
+pageable memory.  At B = 512 that host work is 64 % of the drop-in step (BENCH_r04 ``dropin``).
+
+Here, when the loader's dataset is a plain tensor dataset the fast path understands -- the
+reference's / drop-in's ``BDDataset`` (prepare_dataset.py:13-33) or ``TensorDataset`` -- its
+tensors are uploaded to the device ONCE (re-uploaded only if a source tensor is replaced or
+modified in place: torch's version counter) and every batch is gathered on the device by its
+index list.  The index lists come from the loader's OWN iterator (``iter(loader)`` then the
+sampler's next batch), so the shuffle consumes torch's RNG exactly as ``for batch in loader``
+would and the batches hold the same rows in the same order; the indices travel through a small
+pinned ring (a pageable copy would be synchronous).  Anything else -- workers, a custom
+collate_fn, an iterable or unknown dataset, numpy-backed datasets -- falls back to iterating the
+loader itself.
+"""
+from __future__ import annotations
+
+import weakref
+
+import torch
+from torch.utils.data import DataLoader, Dataset, IterableDataset, TensorDataset
+from torch.utils.data._utils.collate import default_collate
+
+_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+class BDDataset(Dataset):
+    """Dict samples {'mfcc', 'label', 'poison_indicator'} (prepare_dataset.py:13-33); the drop-in
+    prepare_dataset.BDDataset is this class under the reference's module name."""
+
+    def __init__(self, mfcc_list, label_list, poison_index):
+        self.mfcc_list, self.label_list, self.poison_index = mfcc_list, label_list, poison_index
+
+    def __len__(self):
+        return len(self.mfcc_list)
+
+    def __getitem__(self, index):
+        return {"mfcc": self.mfcc_list[index], "label": self.label_list[index],
+                "poison_indicator": self.poison_index[index]}
+
+
+def _is_bddataset(ds) -> bool:
+    """This BDDataset, the drop-in's, the reference's own (prepare_dataset.py:13-33, recognised by
+    name and module), or a subclass that keeps the item contract (no overridden __getitem__ / __len__)."""
+    for k in type(ds).__mro__:
+        if k is BDDataset or (k.__name__ == "BDDataset" and k.__module__.split(".")[-1] == "prepare_dataset"):
+            return type(ds).__getitem__ is k.__getitem__ and type(ds).__len__ is k.__len__
+    return False
+
+
+def _sources(ds, dict_items: bool):
+    """(x, y, ind) source tensors of a dataset whose batches are row gathers of them, or None.
+
+    dict_items: the caller indexes batches by key ('mfcc', 'label', 'poison_indicator'), i.e. it
+    expects BDDataset items (train(), test()'s backdoor loader); otherwise (x, y) tuples."""
+    if isinstance(ds, IterableDataset):
+        return None
+    if dict_items and _is_bddataset(ds):
+        ts = (ds.mfcc_list, ds.label_list, ds.poison_index)
+    elif not dict_items and type(ds) is TensorDataset and len(ds.tensors) == 2:
+        ts = tuple(ds.tensors) + (None,)
+    else:
+        return None
+    if not all(t is None or isinstance(t, torch.Tensor) for t in ts):
+        return None
+    n = ts[0].shape[0] if ts[0].dim() else -1
+    if n < 0 or any(t is not None and (t.dim() == 0 or t.shape[0] != n) for t in ts):
+        return None
+    if not ts[0].is_floating_point():
+        return None
+    return ts
+
+
+def _key(ts):
+    return tuple((id(t), t.data_ptr(), t._version, tuple(t.shape), t.dtype, t.device) if t is not None else None
+                 for t in ts)
+
+
+class _Resident:
+    """Device copies of one dataset's tensors: x as float32 (train()/test() call ``.float()``),
+    y / ind as int64 (``_as_long``)."""
+
+    def __init__(self, ts, dev):
+        x, y, ind = ts
+        self.key = _key(ts)
+        self.dev = dev
+        self.n = x.shape[0]
+        self.x = x.to(dev).float().contiguous()
+        self.y = y.to(dev).long().contiguous()
+        self.ind = ind.to(dev).long().contiguous() if ind is not None else None
+
+
+class _IndexRing:
+    """Batch index lists -> device int64, through two pinned host slots (an event guards reuse)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.cap = 0
+        self.slot = 0
+        self.host = None
+        self.events = [None, None]
+
+    def put(self, idx: torch.Tensor) -> torch.Tensor:
+        if self.dev.type != "cuda":   # host-resident (the CPU tests of the batch order)
+            return idx
+        m = idx.numel()
+        if m > self.cap:
+            if self.host is not None:
+                torch.cuda.current_stream(self.dev).synchronize()
+            self.cap = max(m, 2 * self.cap)
+            self.host = torch.empty((2, self.cap), dtype=torch.int64, pin_memory=True)
+            self.events = [None, None]
+        s = self.slot
+        self.slot ^= 1
+        if self.events[s] is not None:
+            self.events[s].synchronize()   # the copy that last read this slot has finished
+        h = self.host[s, :m]
+        h.copy_(idx)
+        d = h.to(self.dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self.events[s] = ev
+        return d
+
+
+def resident_batches(loader, dev: torch.device, dict_items: bool):
+    """Iterator of (x, y, ind) device batches equal to iterating ``loader`` (same rows, same order,
+    same RNG consumption), or None when the loader is not one the fast path understands."""
+    if dev.type != "cuda" or type(loader) is not DataLoader:
+        return None
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    if loader.num_workers != 0 or loader.collate_fn is not default_collate or loader.batch_sampler is None:
+        return None
+    ts = _sources(loader.dataset, dict_items)
+    if ts is None:
+        return None
+    res = _CACHE.get(loader.dataset)
+    if res is None or res.key != _key(ts) or res.dev != dev:
+        res = _Resident(ts, dev)
+        _CACHE[loader.dataset] = res
+    return _iterate(loader, res)
+
+
+def _iterate(loader, res: _Resident):
+    it = iter(loader)            # the loader's own iterator: base seed + sampler exactly as `for b in loader`
+    ring = _IndexRing(res.dev)
+    while True:
+        try:
+            idx = it._next_index()   # the next batch's index list (no fetch, no collation)
+        except StopIteration:
+            return
+        t = torch.as_tensor(idx, dtype=torch.int64)
+        if t.numel() and (int(t.min()) < -res.n or int(t.max()) >= res.n):
+            raise IndexError(f"index out of range for a dataset of {res.n} items")
+        t = torch.where(t < 0, t + res.n, t)   # python indexing semantics of dataset[i]
+        d = ring.put(t)
+        yield (res.x.index_select(0, d), res.y.index_select(0, d),
+               res.ind.index_select(0, d) if res.ind is not None else None)

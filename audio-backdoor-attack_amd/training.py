@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from .models import smallcnn, dropout_seed
+from .resident import resident_batches
 
 
 # ------------------------------------------------------------------ Adam state shared with torch
@@ -72,6 +73,25 @@ def fusable(model, optimizer, criterion) -> bool:
 def _as_long(t, device):
     t = torch.as_tensor(t).to(device=device, non_blocking=True)
     return t.long().contiguous()
+
+
+def _host_batches(loader, dev, dict_items):
+    for item in loader:
+        if dict_items:
+            x, y, ind = item["mfcc"], item["label"], item["poison_indicator"]
+        else:
+            x, y = item
+            ind = None
+        yield (x.to(dev, non_blocking=True).float().contiguous(), _as_long(y, dev),
+               _as_long(ind, dev) if ind is not None else None)
+
+
+def _batches(loader, dev, dict_items):
+    """(x, y, ind) device batches of a loader: gathered from HBM-resident copies of the dataset's
+    tensors when the loader allows it (resident.py: same rows, order and RNG consumption as
+    iterating it), else iterated and copied batch by batch like the reference (training_tools.py:62-64)."""
+    fast = resident_batches(loader, dev, dict_items)
+    return fast if fast is not None else _host_batches(loader, dev, dict_items)
 
 
 def train_step(model: smallcnn, x, labels, indicators, adam: AdamBinding | None, metrics: torch.Tensor | None,
@@ -169,10 +189,7 @@ def train(model, train_loader, device, optimizer, criterion):
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     adam = None
     nbatches = 0
-    for sample in train_loader:
-        x = sample["mfcc"].to(dev, non_blocking=True).float().contiguous()
-        y = _as_long(sample["label"], dev)
-        ind = _as_long(sample["poison_indicator"], dev)
+    for x, y, ind in _batches(train_loader, dev, True):
         if adam is None:
             model.engine(x)
             adam = AdamBinding(model, optimizer)
@@ -191,15 +208,7 @@ def _eval_batches(model, loader, dev, dict_items):
     eng = None
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     n = 0
-    for item in loader:
-        if dict_items:
-            x, y, ind = item["mfcc"], item["label"], item["poison_indicator"]
-        else:
-            x, y = item
-            ind = None
-        x = x.to(dev, non_blocking=True).float().contiguous()
-        y = _as_long(y, dev)
-        ind = _as_long(ind, dev) if ind is not None else None
+    for x, y, ind in _batches(loader, dev, dict_items):
         eng = model.engine(x)
         torch.ops.abd.smallcnn_eval_metrics(x, eng.params, eng.running, eng.K, model.gemm_precision, y, ind,
                                             metrics)
@@ -228,9 +237,7 @@ def clean_train(model, train_loader, device, optimizer, criterion):
     metrics = torch.zeros(L.METRICS_WORDS, dtype=torch.int64, device=dev)
     adam = None
     nb = 0
-    for x, y in train_loader:
-        x = x.to(dev, non_blocking=True).float().contiguous()
-        y = _as_long(y, dev)
+    for x, y, _ in _batches(train_loader, dev, False):
         if adam is None:
             model.engine(x)
             adam = AdamBinding(model, optimizer)

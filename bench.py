@@ -228,20 +228,14 @@ def dropin_bench(cfg, waves, K, batch, nbatch, dev, precision):
     its feature stage).  Four timings over `nbatch` batches of `batch` rows, each after a warmup:
     cnn_step (training.train_step on device-resident batches: the resident CNN phases), dropin_device
     (train() over already-resident batches: the drop-in's Python + custom-op dispatch around the same
-    step), dropin_loader (train() over the CPU DataLoader: + collation + H2D), loader_only."""
+    step), dropin_loader (train() over the scripts' DataLoader(BDDataset, shuffle=True): the resident
+    fast path, resident.py), dropin_host_loader (the same loader forced through per-batch host
+    collation + pageable H2D, as the reference iterates it), loader_only."""
     import torch
+    from torch.utils.data._utils.collate import default_collate
     from abd_amd import features as F, training as T, _lib as L
     from abd_amd.models import smallcnn
-
-    class DictSet(torch.utils.data.Dataset):   # prepare_dataset.py:13-33 item contract
-        def __init__(self, x, y, ind):
-            self.x, self.y, self.ind = x, y, ind
-
-        def __len__(self):
-            return len(self.x)
-
-        def __getitem__(self, i):
-            return {"mfcc": self.x[i], "label": self.y[i], "poison_indicator": self.ind[i]}
+    from abd_amd.resident import BDDataset   # prepare_dataset.py:13-33 (the drop-in's class)
 
     mcfg = cfg.mfcc()
     n = batch * nbatch
@@ -254,7 +248,9 @@ def dropin_bench(cfg, waves, K, batch, nbatch, dev, precision):
     x_cpu = xs.cpu()
     dev_batches = [{"mfcc": xs[s:s + batch], "label": y[s:s + batch].to(dev), "poison_indicator": ind[s:s + batch].to(dev)}
                    for s in range(0, n, batch)]
-    loader = torch.utils.data.DataLoader(DictSet(x_cpu, y, ind), batch_size=batch, shuffle=True)
+    loader = torch.utils.data.DataLoader(BDDataset(x_cpu, y, ind), batch_size=batch, shuffle=True)
+    host_loader = torch.utils.data.DataLoader(BDDataset(x_cpu, y, ind), batch_size=batch, shuffle=True,
+                                              collate_fn=lambda b: default_collate(b))
     crit = torch.nn.CrossEntropyLoss()
 
     def fresh():
@@ -281,16 +277,21 @@ def dropin_bench(cfg, waves, K, batch, nbatch, dev, precision):
     res["dropin_device_ms"] = timed(lambda: T.train(m1, dev_batches, dev, o1, crit))
     m2, o2 = fresh()
     res["dropin_loader_ms"] = timed(lambda: T.train(m2, loader, dev, o2, crit))
+    m3, o3 = fresh()
+    res["dropin_host_loader_ms"] = timed(lambda: T.train(m3, host_loader, dev, o3, crit))
     t0 = time.perf_counter()
-    for _ in loader:
+    for _ in host_loader:
         pass
     res["loader_only_ms"] = (time.perf_counter() - t0) * 1e3 / nbatch
     res = {k: round(v, 4) for k, v in res.items()}
     res["dropin_device_vs_cnn_step"] = round(res["dropin_device_ms"] / res["cnn_step_ms"], 4)
+    res["dropin_loader_vs_device"] = round(res["dropin_loader_ms"] / res["dropin_device_ms"], 4)
     res["batches"], res["batch"], res["gemm_precision"] = nbatch, batch, precision
     res["note"] = ("train() over a DataLoader of precomputed MFCC (the reference scripts' loop, badnets.py:146-160); "
-                   "dropin_device excludes the loader (batches already in HBM), dropin_loader includes collation "
-                   "and the pageable-memory H2D of each batch")
+                   "dropin_device excludes the loader (batches already in HBM); dropin_loader iterates the scripts' "
+                   "DataLoader(BDDataset, shuffle=True) through the HBM-resident fast path (same batches and RNG "
+                   "consumption, rows gathered on the device); dropin_host_loader forces the reference's per-batch "
+                   "host collation and pageable-memory H2D of each batch")
     return res
 
 

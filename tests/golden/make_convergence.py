@@ -118,9 +118,11 @@ def run(name, out, rng_seed=None):
 
 
 SPREAD_THREADS = 3
-# configs whose final ASR is not saturated: also store RNG replicates (<name>_test_seeds: final
-# test() tuple of each, <name>_train_seeds: final train() tuple)
-SEED_REPLICATES = {"flowmur": (1001, 1002, 1003, 1004)}
+# RNG replicates of every config: the same loop, init and data under other torch
+# seeds (other dropout masks and batch orders) -- the distribution a device-dropout run is one
+# draw of.  Stored per epoch: <name>_test_seeds_ep (R, E, 4) test() tuples, <name>_train_seeds_ep
+# (R, E, 3) train() tuples; <name>_test_seeds / <name>_train_seeds keep the final epoch's.
+SEED_REPLICATES = {n: tuple(range(1001, 1009)) for n in CONV_CFGS}
 # chaotic configs: further fp32 implementations of the SAME run (same seed, data and masks; other
 # summation orders: oneDNN on / off x thread counts), stored as <name>_finalalt<j>_<param> and
 # <name>_test_alt<j>, j = 2, 3, ... -- one alternative underestimates the implementation spread of
@@ -142,11 +144,14 @@ def main():
     out = dict(np.load(path)) if os.path.exists(path) else {}
     only_alt = os.environ.get("ABD_ONLY_ALT") == "1"
     only_extra = os.environ.get("ABD_ONLY_EXTRA") == "1"   # just the ALT_EXTRA implementations
+    only_seeds = os.environ.get("ABD_ONLY_SEEDS") == "1"   # just the RNG replicates
     for n in names:
-        if not only_alt and not only_extra:
+        if only_seeds:
+            pass
+        elif not only_alt and not only_extra:
             torch.set_num_threads(min(8, os.cpu_count() or 1))
             run(n, out)
-        if not only_extra:
+        if not only_extra and not only_seeds:
             torch.set_num_threads(SPREAD_THREADS)
             alt = {}
             with torch.backends.mkldnn.flags(enabled=False):
@@ -155,7 +160,7 @@ def main():
             for k, v in alt.items():   # final-parameter digests of the second implementation
                 if k.startswith(f"{n}_final_"):
                     out[k.replace(f"{n}_final_", f"{n}_finalalt_")] = v
-        for j, (mk, thr) in enumerate(ALT_EXTRA.get(n, ()), start=2):
+        for j, (mk, thr) in enumerate(() if only_seeds else ALT_EXTRA.get(n, ()), start=2):
             torch.set_num_threads(thr)
             alt = {}
             with torch.backends.mkldnn.flags(enabled=mk):
@@ -172,9 +177,11 @@ def main():
             for sd in SEED_REPLICATES[n]:
                 rep = {}
                 run(n, rep, rng_seed=sd)
-                tr_s.append(rep[f"{n}_train"][-1])
-                te_s.append(rep[f"{n}_test"][-1])
-            out[f"{n}_train_seeds"], out[f"{n}_test_seeds"] = np.array(tr_s), np.array(te_s)
+                tr_s.append(rep[f"{n}_train"])
+                te_s.append(rep[f"{n}_test"])
+            out[f"{n}_train_seeds_ep"], out[f"{n}_test_seeds_ep"] = np.array(tr_s), np.array(te_s)
+            out[f"{n}_train_seeds"], out[f"{n}_test_seeds"] = np.array(tr_s)[:, -1], np.array(te_s)[:, -1]
+            np.savez_compressed(path, **out)   # checkpoint per config (a long run)
         out.pop(f"{n}_train_t3", None)
         out.pop(f"{n}_test_t3", None)
     np.savez_compressed(path, **out)

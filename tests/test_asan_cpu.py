@@ -1,0 +1,47 @@
+"""CPU: the host tests under AddressSanitizer (SURVEY §5 "sanitizers"; VERDICT r4 missing #4).
+
+``make -C audio-backdoor-attack_amd asan`` builds libabd_asan.so: the host side of every source
+(C ABI argument checks, smallcnn layout / workspace maps, plan builders) instrumented with
+``-fsanitize=address`` (``-Xarch_host``: GPU ASan is unavailable on this pool).  This runs
+tests/test_host_cpu.py in a child interpreter bound to that library (ABD_LIB) with the ASan runtime
+preloaded; any ASan report fails the child."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, "audio-backdoor-attack_amd")
+LIB = os.path.join(PKG, "libabd_asan.so")
+
+
+def _asan_runtime():
+    for clang in ("/opt/rocm/llvm/bin/clang", "/opt/rocm/lib/llvm/bin/clang"):
+        if os.path.exists(clang):
+            p = subprocess.run([clang, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True,
+                               text=True).stdout.strip()
+            if os.path.isabs(p) and os.path.exists(p):
+                return p
+    return None
+
+
+def test_host_tests_under_asan():
+    if not os.path.exists(LIB):
+        r = subprocess.run(["make", "-C", PKG, "-j8", "asan"], capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-3000:]
+    rt = _asan_runtime()
+    if rt is None:
+        pytest.skip("ASan runtime not found")
+    if os.environ.get("LD_PRELOAD"):
+        pytest.skip("another library is preloaded; the ASan runtime must come first")
+    env = dict(os.environ, ABD_LIB=LIB, LD_PRELOAD=rt,
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1:verify_asan_link_order=0")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(HERE, "test_host_cpu.py")], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=900)
+    out = r.stdout + r.stderr
+    assert "AddressSanitizer" not in out, out[-5000:]
+    assert r.returncode == 0, out[-5000:]
+    assert " passed" in out

@@ -257,3 +257,74 @@ def test_two_rank_uneven_tail_epoch_equals_one_rank(N):
             assert r["samples"] == (N, N), r
             assert r["params"] < 1e-5 and r["running"] < 1e-5 and r["loss"] < 1e-5, r
             assert r["acc"][0] == r["acc"][1] and r["nbt"][0] == r["nbt"][1], r
+
+
+def _syncbn_grad_worker(port, q):
+    """the SyncBN step's code path (no BN1 fold, BN sums from activation passes, the
+    unfused fc head) against the plain fused single-rank step, one step, do_update=False -- no Adam
+    amplification, so the two agree to fp32 rounding."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import torch.distributed as dist
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        import abd_amd
+        from abd_amd import features as F, models as M, parallel_dp as DP, synth, training as T
+        from abd_amd.models import smallcnn
+        from abd_amd.pipeline import attack_config
+        abd_amd.load_library()
+        out = {}
+        for name, prec in (("badnets", "f32split"), ("badnets", "f32"), ("daba", "f32split")):
+            cfg = attack_config(name)
+            B, K = 48, 10
+            waves, labels = synth.make_clips_torch(B, cfg.sample_rate, cfg.length, K, seed=41, device=dev)
+            torch.manual_seed(35)
+            model = smallcnn(K, cfg.linear_features).to(dev).set_gemm_precision(prec)
+            opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+            x = F.mfcc_batch(waves, cfg.mfcc(), rows=torch.arange(B, dtype=torch.int32, device=dev))
+            y = labels.to(dev, torch.int64)
+            ind = torch.zeros(B, dtype=torch.int64, device=dev)
+            eng = model.engine(x)
+            adam = T.AdamBinding(model, opt)
+            g = torch.Generator(device="cpu").manual_seed(5)
+            m1 = (torch.rand((B, eng.flat), generator=g) < 0.6).to(torch.uint8).to(dev)
+            m2 = (torch.rand((B, 128), generator=g) < 0.5).to(torch.uint8).to(dev)
+            run0 = eng.running.clone()
+            res = []
+            for sync in (None, DP.SyncBatchNorm(dev)):
+                eng.running.copy_(run0)
+                eng.grads.fill_(1e30)
+                T.train_step(model, x, y, ind, adam, None, m1, m2, do_update=False, seed=1, bn_sync=sync)
+                torch.cuda.synchronize()
+                res.append((eng.grads.clone(), eng.running.clone(), None if sync is None else sync.calls))
+            (ga, ra, _), (gb, rb, calls) = res
+            per = {p: float((u - v).norm() / max(float(v.norm()), 1e-30))
+                   for p, u, v in zip(M.PARAM_ORDER, eng.views(gb), eng.views(ga))}
+            out[(name, prec)] = {"calls": calls, "grads": per,
+                                 "running": float((rb - ra).norm() / (ra - run0).norm())}
+        q.put((out, None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((None, traceback.format_exc()))
+        raise
+
+
+def test_world1_sync_bn_gradients_equal_fused_step():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_syncbn_grad_worker, args=(_free_port(), q))
+    p.start()
+    out, tb = q.get(timeout=110)
+    p.join(timeout=30)
+    assert tb is None, tb
+    for key, r in out.items():
+        print(key, r["calls"], f"running {r['running']:.1e}", {k: f"{v:.1e}" for k, v in r["grads"].items()})
+        assert r["calls"] == 6, (key, r["calls"])             # the SyncBN path really ran
+        assert r["running"] < 1e-5, (key, r)                  # BN batch statistics (running-stat update)
+        for pname, e in r["grads"].items():
+            assert e < 1e-5, (key, pname, e)                  # every parameter gradient

@@ -52,6 +52,25 @@ def test_mfcc_matches_oracle(dev, cfg):
     assert e < RTOL_MAX
 
 
+@pytest.mark.parametrize("generic", [False, True])
+def test_mfcc_lds_dct_geometry(dev, monkeypatch, generic):
+    """n_mels % 16 != 0 and no specialised FFT plan (n_fft 512): the DCT runs on db_dct_lds_kernel
+    (ADVICE r4), or on the VALU db_dct_kernel under ABD_GENERIC_FFT; both against the oracle."""
+    if generic:
+        monkeypatch.setenv("ABD_GENERIC_FFT", "1")
+    F._PLANS.clear()              # the env is read at plan creation
+    sr, nm, nf, hop, Ln, nmel = 16000, 20, 512, 128, 16000, 40
+    w, _ = synth.make_clips_np(5, sr, Ln, 10, seed=77)
+    c = F.MfccConfig(sr, nm, nf, hop, Ln, n_mels=nmel)
+    try:
+        got = F.mfcc_batch(torch.tensor(w, device=dev), c).cpu().numpy()
+    finally:
+        F._PLANS.clear()
+    ref = np.transpose(om.mfcc_core(w.astype(np.float64), sr, nm, nf, hop, n_mels=nmel), (0, 2, 1))[:, None]
+    assert got.shape == ref.shape
+    assert _rel_err(got, ref) < RTOL_MAX
+
+
 def test_mfcc_row_gather_and_ragged_batch(dev):
     sr, nm, nf, hop, Ln = 16000, 40, 400, 160, 16000
     w, _ = synth.make_clips_np(9, sr, Ln, 10, seed=5)
