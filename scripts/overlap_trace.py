@@ -42,7 +42,7 @@ def run(mode, steps):
     import abd_amd
     from abd_amd import synth
     from abd_amd.models import smallcnn
-    from abd_amd.pipeline import ResidentTrainer, attack_config
+    from abd_amd.pipeline import ResidentTrainer, attack_config, ultrasonic_trigger
     abd_amd.load_library()
     cfg = attack_config("ultrasonic")
     B, K = 512, 35
@@ -50,7 +50,8 @@ def run(mode, steps):
     torch.manual_seed(35)
     model = smallcnn(K, cfg.linear_features).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    tr = ResidentTrainer(cfg, waves, labels, model, opt, B, seed=35, rank=0, world=1, collectives=True)
+    tr = ResidentTrainer(cfg, waves, labels, model, opt, B, trigger=ultrasonic_trigger(60, "mid", False), seed=35,
+                         rank=0, world=1, collectives=True)
     red = tr.reducer
     if mode == "surrogate":
         def launch_fc():

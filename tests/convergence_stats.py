@@ -1,0 +1,47 @@
+"""Per-epoch bound for a run that is another DRAW of the reference's training (device dropout, bf16).
+
+Shared by tests/test_gpu_convergence.py (the check) and tests/test_convergence_calibration_cpu.py
+(its false-alarm rate on the reference's own draws).  At every epoch and metric the mean of D draws
+may differ from the mean of the reference's draws by at most
+
+    max(0.5 pp, K_SIGMA * sigma_e * sqrt(1/D + 1/R), 2 samples of the metric's denominator)
+
+with sigma_e the reference draws' standard deviation at that epoch (R draws), floored at
+SIGMA_FLOOR: a metric that all reference draws hit exactly (100 % at a saturated epoch) has
+sample sigma 0, not population sigma 0."""
+import numpy as np
+
+K_SIGMA = 4.0
+SIGMA_FLOOR = 0.5
+
+# (label, source, column, denominator key): test() tuple (clean acc, ASR, clean loss, bd loss),
+# train() tuple (loss, mix acc, ASR)
+METRICS = (("test clean acc", "te", 0, "n_test"), ("test ASR", "te", 1, "n_bd"),
+           ("train acc", "tr", 1, "n_train"), ("train ASR", "tr", 2, "n_pois"))
+
+
+def ref_draws(conv_ref, name):
+    """(R, E, 4) test() tuples and (R, E, 3) train() tuples: the fixture run + its RNG replicates."""
+    te = np.concatenate([conv_ref[f"{name}_test"][None], conv_ref[f"{name}_test_seeds_ep"]])
+    tr = np.concatenate([conv_ref[f"{name}_train"][None], conv_ref[f"{name}_train_seeds_ep"]])
+    return te, tr
+
+
+def draw_bound(ref_vals, n_dev, n_den):
+    """ref_vals (R, E): allowed |mean of n_dev draws - mean of ref_vals| per epoch (pp)."""
+    sig = np.maximum(ref_vals.std(axis=0, ddof=1), SIGMA_FLOOR)
+    se = sig * np.sqrt(1.0 / n_dev + 1.0 / ref_vals.shape[0])
+    return np.maximum(np.maximum(0.5, K_SIGMA * se), 200.0 / n_den)
+
+
+def violations(ours_te, ours_tr, ref_te, ref_tr, dens):
+    """[(metric, epoch, ours, ref mean, bound)] outside the bound; ours_* (D, E, ...)."""
+    bad = []
+    srcs = {"te": (ours_te, ref_te), "tr": (ours_tr, ref_tr)}
+    for what, src, col, den in METRICS:
+        o, r = srcs[src][0][:, :, col], srcs[src][1][:, :, col]
+        bound = draw_bound(r, o.shape[0], dens[den])
+        gap = np.abs(o.mean(0) - r.mean(0))
+        for e in np.nonzero(gap > bound)[0]:
+            bad.append((what, int(e) + 1, float(o[:, e].mean()), float(r[:, e].mean()), float(bound[e])))
+    return bad
