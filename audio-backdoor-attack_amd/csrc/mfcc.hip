@@ -808,6 +808,10 @@ struct DftV<16> {
   static __device__ __forceinline__ void run(f2v* v) { dftv_comp<4, 4>(v); }
 };
 template <>
+struct DftV<20> {
+  static __device__ __forceinline__ void run(f2v* v) { dftv_comp<4, 5>(v); }
+};
+template <>
 struct DftV<25> {
   static __device__ __forceinline__ void run(f2v* v) { dftv_comp<5, 5>(v); }
 };
@@ -1410,7 +1414,7 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
 // NBLK: blocks per CU the Bluestein build is register-budgeted for (8: 64 VGPRs and <= 80 SGPRs, the
 // compiler spills SGPRs into VGPR lanes; 7: 72 VGPRs / 96 SGPRs, no spills, one block fewer)
 template <int M, int NN, int R0, int R1, int R2, int PP, bool BLUE, int NBLK = kBlueBlocks>
-__global__ void __launch_bounds__(kThreads, BLUE ? NBLK : 1) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
+__global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p, const float* __restrict__ wave,
                                                                  int64_t row_stride,
                                                                  const int32_t* __restrict__ rows, int64_t batch,
                                                                  InjDev inj, const float* __restrict__ rowscale,
@@ -1843,8 +1847,27 @@ struct FastPlan {
 #define ABD_BLUE_R1 12
 #endif
 constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (ABD_BLUE_R0 * ABD_BLUE_R1);
-constexpr FastPlan kFastPlans[] = {
-    {2304, 1103, 1, 1, kBlueR0, kBlueR1}, {2048, 2048, 0, 4, 16, 16}, {400, 400, 0, 13, 16, 25}};
+// 2048-point (FlowMur / DABA) and 400-point (BadNets / JingleBack) plans: frame pairs per item and
+// blocks per CU the build is register-budgeted for (measurement builds override them)
+#ifndef ABD_F2048_PP
+#define ABD_F2048_PP 4
+#endif
+#ifndef ABD_F2048_NBLK
+#define ABD_F2048_NBLK 1
+#endif
+#ifndef ABD_F400_PP
+#define ABD_F400_PP 13
+#endif
+#ifndef ABD_F400_R0
+#define ABD_F400_R0 16
+#endif
+#ifndef ABD_F400_NBLK
+#define ABD_F400_NBLK 1
+#endif
+constexpr int kF400R0 = ABD_F400_R0, kF400R1 = 400 / ABD_F400_R0;
+constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1, kBlueR0, kBlueR1},
+                                   {2048, 2048, 0, ABD_F2048_PP, 16, 16},
+                                   {400, 400, 0, ABD_F400_PP, kF400R0, kF400R1}};
 
 const FastPlan* find_fast(int M, int N, int blue) {
   for (const auto& f : kFastPlans)
@@ -1901,11 +1924,12 @@ int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const
     return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
                                                        queue, s);
   if (d.M == 2048 && d.N == 2048 && !d.bluestein)
-    return launch_fast<2048, 2048, 16, 16, 8, 4, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db,
-                                                        ws_max, queue, s);
+    return launch_fast<2048, 2048, 16, 16, 8, ABD_F2048_PP, false, ABD_F2048_NBLK>(d, wave, row_stride, rows, batch, ij,
+                                                                                  rowscale, ws_db, ws_max, queue, s);
   if (d.M == 400 && d.N == 400 && !d.bluestein)
-    return launch_fast<400, 400, 16, 25, 1, 13, false>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
-                                                       queue, s);
+    return launch_fast<400, 400, kF400R0, kF400R1, 1, ABD_F400_PP, false, ABD_F400_NBLK>(d, wave, row_stride, rows, batch,
+                                                                                         ij, rowscale, ws_db, ws_max,
+                                                                                         queue, s);
   return -1;
 }
 
