@@ -80,6 +80,12 @@ struct MfccDev {
   const float* mel2_w;    // compact slot weights
   int mel2_total, mel2_hp;  // #weights, max slot count rounded up to 8
   const float* mel3_w;      // Bluestein fast path: kMelHP zero-padded weights per slot (NULL = unused)
+  // non-Bluestein fast path: every filter's support cut into segments of <= kMelSeg bins (a segment
+  // near the top shifted down so its kMelSeg reads stay below n_freqs, its weights offset to match)
+  const int* mseg_start;    // first bin read by segment s
+  const float4* mseg_w;     // [s][kMelSeg / 4] zero-padded weights
+  const int2* mfilt_seg;    // filter m: (first segment, segment count)
+  int nseg;                 // segments (0 = use the half-slot loop)
   // backward (mel^T): the <= 2 filters that touch each bin (-1 = none) and their weights
   const int2* bin_mel;
   const float2* bin_w;
@@ -1345,6 +1351,14 @@ constexpr int kBlueBlocks = 8;
 //          per slot (p.mel3_w), every read base + immediate, one float2 FMA per bin for both
 //          frames (two v_fma_f32 in the scalar build); the halves are combined by a lane swap, lane h writes frame 2 p0 + h.
 constexpr int kMelHP = 16;  // padded bins per half-filter slot of the Bluestein fast path
+// bins per mel segment of the non-Bluestein fast path (MfccDev::mseg_*); ABD_MEL_SEG=0 builds the
+// half-slot loop instead (measurement builds)
+constexpr int kMelSeg = 8;
+#ifndef ABD_MEL_SEG
+#define ABD_MEL_SEG 1
+#endif
+// float2 slot of a pair's FFT buffer where the segmented mel's partials start (past pidx(nf - 1))
+constexpr int mel_seg_offset(int nf) { return ((nf + nf / 16) + 15) / 16 * 16; }
 template <int M, int NN>
 __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const MfccDev& p, float* __restrict__ db_u,
                                                 int t0) {
@@ -1523,38 +1537,82 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
         Z[pidx(k)] = make_float2(ar * ar + ai * ai, br * br + bi * bi);
       }
       __syncthreads();
-      const int tot = np * S;
-      const int rounds = (tot + kThreads - 1) / kThreads;
-      const int hp = p.mel2_hp;
-      const int wlast = p.mel2_total - 1;
-      for (int rd = 0; rd < rounds; ++rd) {  // uniform: every lane reaches the shuffles
-        const int g = ltid() + rd * kThreads;
-        const bool act = g < tot;
-        const int gg = act ? g : 0;
-        const int f = gg / S;
-        const int sl = gg - f * S;
-        const int4 meta = p.mel2_meta[sl];  // (start, count, weight offset, -)
-        const float2* Z = buf + f * (M + M / 16);
-        float sa = 0.0f, sb = 0.0f;
-        for (int i0 = 0; i0 < hp; i0 += 8) {
+      if (p.nseg > 0) {
+        // segmented mel (MfccDev::mseg_*): task = (pair f, segment) -> the segment's kMelSeg bins
+        // of both frames into a partial past the power values (Z[k > N/2] is dead after the power
+        // stage), then task = (pair f, filter m) sums its segments in order -> dB of both frames
+        constexpr int PSO = mel_seg_offset(nf);
+        const int nseg = p.nseg;
+        for (int g = ltid(); g < np * nseg; g += kThreads) {
+          const int f = g / nseg, sg = g - f * nseg;
+          const float2* Z = buf + f * (M + M / 16);
+          const int st = p.mseg_start[sg];
+          f2v acc = f2v{0.0f, 0.0f};
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int i = i0 + q;
-            const int k = min(meta.x + i, nf - 1);
-            const float w = (i < meta.y) ? wl[min(meta.z + i, wlast)] : 0.0f;
-            const float2 pw = Z[pidx(k)];
-            sa = fmaf(pw.x, w, sa);
-            sb = fmaf(pw.y, w, sb);
+          for (int q = 0; q < kMelSeg / 4; ++q) {
+            const float4 w4 = p.mseg_w[sg * (kMelSeg / 4) + q];
+            const float wq[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float2 pw = Z[pidx(st + 4 * q + e)];
+              acc = fmav(f2v{pw.x, pw.y}, f2v{wq[e], wq[e]}, acc);
+            }
+          }
+          reinterpret_cast<f2v*>(buf + f * (M + M / 16) + PSO)[sg] = acc;
+        }
+        __syncthreads();
+        for (int h = ltid(); h < np * p.n_mels; h += kThreads) {
+          const int f = h / p.n_mels, m = h - f * p.n_mels;
+          const f2v* part = reinterpret_cast<const f2v*>(buf + f * (M + M / 16) + PSO);
+          const int2 fs = p.mfilt_seg[m];
+          f2v sum = part[fs.x];
+          for (int j = 1; j < fs.y; ++j) sum += part[fs.x + j];
+          const int t = 2 * (p0 + f);
+          if (t < p.T) {
+            const float d = 10.0f * log10f(fmaxf(sum.x, 1e-10f));
+            ws_db[((int64_t)u * p.T + t) * p.n_mels + m] = d;
+            lmax = fmaxf(lmax, d);
+          }
+          if (t + 1 < p.T) {
+            const float d = 10.0f * log10f(fmaxf(sum.y, 1e-10f));
+            ws_db[((int64_t)u * p.T + t + 1) * p.n_mels + m] = d;
+            lmax = fmaxf(lmax, d);
           }
         }
-        sa += __shfl_xor(sa, 1);
-        sb += __shfl_xor(sb, 1);
-        const int h = sl & 1;
-        const int t = 2 * (p0 + f) + h;
-        if (act && t < p.T) {
-          const float d = 10.0f * log10f(fmaxf(h ? sb : sa, 1e-10f));
-          ws_db[((int64_t)u * p.T + t) * p.n_mels + (sl >> 1)] = d;
-          lmax = fmaxf(lmax, d);
+      } else {
+        const int tot = np * S;
+        const int rounds = (tot + kThreads - 1) / kThreads;
+        const int hp = p.mel2_hp;
+        const int wlast = p.mel2_total - 1;
+        for (int rd = 0; rd < rounds; ++rd) {  // uniform: every lane reaches the shuffles
+          const int g = ltid() + rd * kThreads;
+          const bool act = g < tot;
+          const int gg = act ? g : 0;
+          const int f = gg / S;
+          const int sl = gg - f * S;
+          const int4 meta = p.mel2_meta[sl];  // (start, count, weight offset, -)
+          const float2* Z = buf + f * (M + M / 16);
+          float sa = 0.0f, sb = 0.0f;
+          for (int i0 = 0; i0 < hp; i0 += 8) {
+  #pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const int i = i0 + q;
+              const int k = min(meta.x + i, nf - 1);
+              const float w = (i < meta.y) ? wl[min(meta.z + i, wlast)] : 0.0f;
+              const float2 pw = Z[pidx(k)];
+              sa = fmaf(pw.x, w, sa);
+              sb = fmaf(pw.y, w, sb);
+            }
+          }
+          sa += __shfl_xor(sa, 1);
+          sb += __shfl_xor(sb, 1);
+          const int h = sl & 1;
+          const int t = 2 * (p0 + f) + h;
+          if (act && t < p.T) {
+            const float d = 10.0f * log10f(fmaxf(h ? sb : sa, 1e-10f));
+            ws_db[((int64_t)u * p.T + t) * p.n_mels + (sl >> 1)] = d;
+            lmax = fmaxf(lmax, d);
+          }
         }
       }
     }
@@ -1848,21 +1906,25 @@ struct FastPlan {
 #endif
 constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (ABD_BLUE_R0 * ABD_BLUE_R1);
 // 2048-point (FlowMur / DABA) and 400-point (BadNets / JingleBack) plans: frame pairs per item and
-// blocks per CU the build is register-budgeted for (measurement builds override them)
+// blocks per CU the build is register-budgeted for (measurement builds override them).  Round 5
+// (scripts/stft_plan_ab.sh, feature stage at B = 256, two alternations on one box): 2048 points
+// PP 4 / 1 block-budget 0.0495 ms -> PP 2 / 4 blocks 0.0437 (PP 1: 0.058, PP 3: 0.051); 400 points
+// PP 13 / 1 0.0590 -> PP 8 / 4 0.0504 (PP 6: 0.055, 9: 0.052, 10: 0.054, 17: 0.066; a 20 x 20
+// radix plan at PP 12: 0.058).  Both also take the segmented mel (0.0705 / 0.0576 before it).
 #ifndef ABD_F2048_PP
-#define ABD_F2048_PP 4
+#define ABD_F2048_PP 2
 #endif
 #ifndef ABD_F2048_NBLK
-#define ABD_F2048_NBLK 1
+#define ABD_F2048_NBLK 4
 #endif
 #ifndef ABD_F400_PP
-#define ABD_F400_PP 13
+#define ABD_F400_PP 8
 #endif
 #ifndef ABD_F400_R0
 #define ABD_F400_R0 16
 #endif
 #ifndef ABD_F400_NBLK
-#define ABD_F400_NBLK 1
+#define ABD_F400_NBLK 4
 #endif
 constexpr int kF400R0 = ABD_F400_R0, kF400R1 = 400 / ABD_F400_R0;
 constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1, kBlueR0, kBlueR1},
@@ -1951,10 +2013,12 @@ int launch_stft_bwd(const MfccDev& d, const float* wave, int64_t row_stride, con
 
 int dispatch_stft_bwd(const MfccDev& d, const float* wave, int64_t row_stride, const int32_t* rows, int64_t batch,
                       const InjDev& ij, const float* rowscale, const float* dmel, float* gframes, hipStream_t s) {
-  if (d.M == 2048 && d.N == 2048 && !d.bluestein && d.ppb == 4)
-    return launch_stft_bwd<2048, 16, 16, 8, 4>(d, wave, row_stride, rows, batch, ij, rowscale, dmel, gframes, s);
-  if (d.M == 400 && d.N == 400 && !d.bluestein && d.ppb == 13)
-    return launch_stft_bwd<400, 16, 25, 1, 13>(d, wave, row_stride, rows, batch, ij, rowscale, dmel, gframes, s);
+  if (d.M == 2048 && d.N == 2048 && !d.bluestein && d.ppb == ABD_F2048_PP)
+    return launch_stft_bwd<2048, 16, 16, 8, ABD_F2048_PP>(d, wave, row_stride, rows, batch, ij, rowscale, dmel, gframes,
+                                                          s);
+  if (d.M == 400 && d.N == 400 && !d.bluestein && d.ppb == ABD_F400_PP)
+    return launch_stft_bwd<400, kF400R0, kF400R1, 1, ABD_F400_PP>(d, wave, row_stride, rows, batch, ij, rowscale, dmel,
+                                                                  gframes, s);
   return -1;
 }
 
@@ -2226,6 +2290,33 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
     for (int sl = 0; sl < 2 * n_mels; ++sl)
       for (int i = 0; i < meta2[sl].y; ++i)
         mw3[(((size_t)(i / 4) * (2 * n_mels) + sl) * 4) + (i % 4)] = mw2[meta2[sl].z + i];
+  // segmented mel for the non-Bluestein fast kernel: filter m's support [lo, lo + cnt) as
+  // ceil(cnt / kMelSeg) segments (one for an empty filter), summed per filter in segment order
+  bool mseg = !blue && d.fast && nf >= kMelSeg && ABD_MEL_SEG;
+  std::vector<int> seg_start;
+  std::vector<float> seg_w;
+  std::vector<int2> filt_seg(mseg ? n_mels : 0);
+  if (mseg)
+    for (int m = 0; m < n_mels; ++m) {
+      const int lo = mstart[m], cnt = mcount[m];
+      const int ns = std::max(1, (cnt + kMelSeg - 1) / kMelSeg);
+      filt_seg[m] = make_int2((int)seg_start.size(), ns);
+      for (int g = 0; g < ns; ++g) {
+        const int b0 = lo + g * kMelSeg, c = std::max(0, std::min(kMelSeg, cnt - g * kMelSeg));
+        const int st = std::min(b0, nf - kMelSeg);  // reads st .. st + kMelSeg - 1 < nf
+        seg_start.push_back(st);
+        for (int i = 0; i < kMelSeg; ++i) {
+          const int k = st + i;
+          seg_w.push_back((k >= b0 && k < b0 + c) ? (float)fb[(size_t)k * n_mels + m] : 0.0f);
+        }
+      }
+    }
+  if (mseg && mel_seg_offset(nf) + (int)seg_start.size() > M + M / 16) {  // partials must fit the buffer
+    mseg = false;
+    seg_start.clear();
+    seg_w.clear();
+    filt_seg.clear();
+  }
   // fast-kernel twiddles: W_{R0 R1}^e and W_M^k, e, k < R0 R1
   const int r01 = fp ? fp->r0 * fp->r1 : 1;
   std::vector<float2> ftw(2 * (size_t)r01);
@@ -2344,6 +2435,12 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   sz += al(mw2.size() * sizeof(float));
   size_t off_w3 = sz;
   sz += al(mw3.size() * sizeof(float));
+  size_t off_sst = sz;
+  sz += al(seg_start.size() * sizeof(int));
+  size_t off_sw = sz;
+  sz += al(seg_w.size() * sizeof(float));
+  size_t off_fs = sz;
+  sz += al(filt_seg.size() * sizeof(int2));
   size_t off_bm = sz;
   sz += al(nf * sizeof(int2));
   size_t off_bw = sz;
@@ -2370,6 +2467,11 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   memcpy(&host[off_m2], meta2.data(), meta2.size() * sizeof(int4));
   memcpy(&host[off_w2], mw2.data(), mw2.size() * sizeof(float));
   if (!mw3.empty()) memcpy(&host[off_w3], mw3.data(), mw3.size() * sizeof(float));
+  if (mseg) {
+    memcpy(&host[off_sst], seg_start.data(), seg_start.size() * sizeof(int));
+    memcpy(&host[off_sw], seg_w.data(), seg_w.size() * sizeof(float));
+    memcpy(&host[off_fs], filt_seg.data(), filt_seg.size() * sizeof(int2));
+  }
   hipError_t e = hipMalloc(&pl->block, sz);
   if (e != hipSuccess) {
     delete pl;
@@ -2403,6 +2505,10 @@ int abd_mfcc_plan_create(int sample_rate, int n_fft, int hop_length, int n_mels,
   d.mel2_meta = reinterpret_cast<const int4*>(b + off_m2);
   d.mel2_w = reinterpret_cast<const float*>(b + off_w2);
   d.mel3_w = mw3.empty() || generic ? nullptr : reinterpret_cast<const float*>(b + off_w3);
+  d.mseg_start = mseg ? reinterpret_cast<const int*>(b + off_sst) : nullptr;
+  d.mseg_w = mseg ? reinterpret_cast<const float4*>(b + off_sw) : nullptr;
+  d.mfilt_seg = mseg ? reinterpret_cast<const int2*>(b + off_fs) : nullptr;
+  d.nseg = mseg ? (int)seg_start.size() : 0;
   d.bin_mel = reinterpret_cast<const int2*>(b + off_bm);
   d.bin_w = reinterpret_cast<const float2*>(b + off_bw);
   *plan = pl;
