@@ -4290,10 +4290,11 @@ int ws_grid() {
 // only one).  Small problems (FlowMur's 32 x 13 input: conv2 has 23 k rows at B = 256) get no more
 // blocks than give every wave one 32-row tile: each block stages the whole weight operand into its
 // LDS, so the full grid would stage it 256 times for ~11 rows per wave.
-int ws_blocks(int N, int Cs, int64_t M) {
-  (void)N;
-  (void)Cs;
-  const int64_t need = (M + 8 * 32 - 1) / (8 * 32);  // 8-wave blocks
+// rows_per_block: 32 per computing wave -- 8 for the split / DMA / pre-split kernels, 4 for the
+// wave-specialised kernel (4 consumers + 4 producers; round 5: FlowMur's conv3 forward, M = 3,840,
+// ran 15 blocks of two serial tiles per consumer instead of 30 of one)
+int ws_blocks(int64_t M, int rows_per_block = 8 * 32) {
+  const int64_t need = (M + rows_per_block - 1) / rows_per_block;
   return (int)std::max<int64_t>(1, std::min<int64_t>(ws_grid(), need));
 }
 // 32-bit buffer offsets of the weight-stationary kernels (their A operand is one buffer resource)
@@ -4336,20 +4337,11 @@ int dma_span(const NTArgs& a) {
   cache[key] = span;
   return span;
 }
-template <int EPI, int NP = 3, bool PA = false>
-int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
-  if (!ws_fits(a)) return -1;
-  if (PA && (a.srcs == nullptr || a.N != 64 || a.Cs != 64)) return -1;
-  const int nb = ws_blocks(a.N, a.Cs, a.M);
-  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
-  if (phase >= 0) abd::prof_begin(phase, s);
-  // K-step order (see the kernel): channel-group-major for the forward (conv2 0.147 -> 0.141 ms),
-  // tap-major for the data gradient (0.133 vs 0.136 ms channel-major)
-  const bool ko = EPI == EPI_CONV;
-  // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the f32split data
-  // gradient measured no faster through it (r4_v4: 0.1309 direct vs 0.1316 staged), so it stays on
-  // the direct kernel by default (ws_dma_mode); bf16's plane-operand data gradient is staged
-  // (0.0702 -> 0.0683 ms)
+// Which weight-stationary kernel launch_conv_ws_split takes for these arguments (its grid -- and
+// EPI_CONV's partial count a.nblk -- depends on it: ws_nblk)
+enum WsKind { WS_SPEC, WS_PRE, WS_DMA, WS_SPLIT };
+template <int EPI, int NP, bool PA>
+WsKind ws_kind(const NTArgs& a) {
   const int dma_mode = ws_dma_mode();
   const bool dma = dma_mode == 2 || (dma_mode == 1 && (EPI == EPI_CONV || (PA && NP == 1) ||
                                                       (ABD_WS_PRE >= 2 && NP == 3 && !PA && a.N == 64)));
@@ -4358,16 +4350,41 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
                         a.dh[3] == 1 && a.dw[3] == 1 && a.Hs == a.Ho + 1 && a.Ws == a.Wo + 1;
   const bool dg_taps = a.dh[0] == 0 && a.dw[0] == 0 && a.dh[1] == 0 && a.dw[1] == -1 && a.dh[2] == -1 && a.dw[2] == 0 &&
                        a.dh[3] == -1 && a.dw[3] == -1;
-  // conv3 (N = 32) through the same kernel with one 32-column tile per wave; bf16's plane operands
-  // (PA, conv2) staged as bf16
   if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
     constexpr bool spec = ABD_WS_SPEC >= 2 || (ABD_WS_SPEC == 1 && EPI == EPI_CONV);
+    if (PA && NP == 1) return WS_DMA;
+    if (NP == 3 && a.N == 64 && ABD_WS_PRE) return spec ? WS_SPEC : WS_PRE;
+    if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) return spec ? WS_SPEC : WS_PRE;
+    return WS_DMA;
+  }
+  return WS_SPLIT;
+}
+template <int EPI, int NP, bool PA>
+int ws_nblk(const NTArgs& a) {
+  return ws_blocks(a.M, ws_kind<EPI, NP, PA>(a) == WS_SPEC ? 4 * 32 : 8 * 32);
+}
+template <int EPI, int NP = 3, bool PA = false>
+int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
+  if (!ws_fits(a)) return -1;
+  if (PA && (a.srcs == nullptr || a.N != 64 || a.Cs != 64)) return -1;
+  const WsKind kind = ws_kind<EPI, NP, PA>(a);
+  const int nb = ws_blocks(a.M, kind == WS_SPEC ? 4 * 32 : 8 * 32);
+  if (EPI == EPI_CONV && a.part != nullptr && a.nblk != nb) return -1;
+  if (phase >= 0) abd::prof_begin(phase, s);
+  // K-step order (see the kernel): channel-group-major for the forward (conv2 0.147 -> 0.141 ms),
+  // tap-major for the data gradient (0.133 vs 0.136 ms channel-major)
+  const bool ko = EPI == EPI_CONV;
+  // LDS-DMA A operand (conv_ws_dma_kernel): the forward 0.140 -> 0.130-0.134 ms; the f32split data
+  // gradient measured no faster through it (r4_v4: 0.1309 direct vs 0.1316 staged), so it stays on
+  // the direct kernel by default (ws_dma_mode); bf16's plane-operand data gradient is staged
+  // (0.0702 -> 0.0683 ms).  conv3 (N = 32) runs the same kernels with one 32-column tile per wave.
+  if (kind != WS_SPLIT) {
     if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 64 && ABD_WS_PRE && spec) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3 && spec) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 64 && ABD_WS_PRE) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (kind == WS_SPEC && a.N == 64) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (kind == WS_SPEC) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (kind == WS_PRE && a.N == 64) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    else if (kind == WS_PRE) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (a.N == 64) conv_ws_dma_kernel<EPI, NP><<<dim3(nb), dim3(512), 0, s>>>(a);
     else conv_ws_dma_kernel<EPI, NP, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
   } else if (PA) {
@@ -4583,17 +4600,19 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     // f32split / bf16: the weight-stationary kernels (bf16 on one plane); fp32 MFMA otherwise, and
     // for a batch past their 32-bit buffer offsets
     const bool ws = (sp || bf) && ws_fits(a);
-    a.nblk = ws ? ws_blocks(64, 64, a.M) : nt_grid_x<64, EPI_CONV>(a);
+    if (planes > 0) {   // (set before the grid: the plane-operand kernel takes its own grid)
+      a.srcs = w.p1s;
+      a.splane = B * g.H1 * g.W1p * 64;
+    }
+    a.nblk = !ws ? nt_grid_x<64, EPI_CONV>(a)
+             : planes == 1 ? ws_nblk<EPI_CONV, 1, true>(a)
+             : bf ? ws_nblk<EPI_CONV, 1, false>(a) : ws_nblk<EPI_CONV, 3, false>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     // p1 holds m under the BN1 fold: only the weight-stationary split kernel applies it (bn1_fold_ok)
     ABD_CHECK(!fold1 || ws, ABD_E_UNSUPPORTED, "BN1 fold needs the weight-stationary conv2 kernel");
     if (fold1) {
       a.Bw = w.w2fold;
       a.fold_t = w.ft2;
-    }
-    if (planes > 0) {
-      a.srcs = w.p1s;
-      a.splane = B * g.H1 * g.W1p * 64;
     }
     if (planes == 1 ? launch_conv_ws_split<EPI_CONV, 1, true>(a, s, abd::PH_CONV2_FWD)
         : ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
@@ -4625,7 +4644,7 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     NTArgs a = conv_fwd_args(w.p2, g.H2p, g.W2p, 64, g.H3, g.W3, B, w.w3f, 32, P.p[P_C3B], w.r3);
     const bool bf3 = net->precision == ABD_PREC_BF16, sp3 = net->precision == ABD_PREC_F32_SPLIT;
     const bool ws3 = (sp3 || bf3) && ws_fits(a);
-    a.nblk = ws3 ? ws_blocks(32, 64, a.M) : nt_grid_x<32, EPI_CONV>(a);
+    a.nblk = !ws3 ? nt_grid_x<32, EPI_CONV>(a) : bf3 ? ws_nblk<EPI_CONV, 1, false>(a) : ws_nblk<EPI_CONV, 3, false>(a);
     a.part = (train && !inst) ? w.part : nullptr;
     if (ws3 ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
                    : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))

@@ -8,11 +8,17 @@ may differ from the mean of the reference's draws by at most
 
 with sigma_e the reference draws' standard deviation at that epoch (R draws), floored at
 SIGMA_FLOOR: a metric that all reference draws hit exactly (100 % at a saturated epoch) has
-sample sigma 0, not population sigma 0."""
+sample sigma 0, not population sigma 0.  Many epoch-metric cells are compared per run and a run's
+epochs are correlated (a draw that learns the poisoned subset early stays ahead), so the rule allows
+at most MAX_CELLS cells past the bound and none past MAX_RATIO times it; calibrated on the reference's
+own draws (tests/test_convergence_calibration_cpu.py: 0 of 420 leave-3-out splits fail it, against
+4 of 420 for "at most one cell")."""
 import numpy as np
 
 K_SIGMA = 4.0
 SIGMA_FLOOR = 0.5
+MAX_CELLS = 2
+MAX_RATIO = 2.0
 
 # (label, source, column, denominator key): test() tuple (clean acc, ASR, clean loss, bd loss),
 # train() tuple (loss, mix acc, ASR)
@@ -45,3 +51,8 @@ def violations(ours_te, ours_tr, ref_te, ref_tr, dens):
         for e in np.nonzero(gap > bound)[0]:
             bad.append((what, int(e) + 1, float(o[:, e].mean()), float(r[:, e].mean()), float(bound[e])))
     return bad
+
+
+def rule_fails(bad):
+    """True when the violations list breaks the per-run rule (MAX_CELLS, MAX_RATIO)."""
+    return len(bad) > MAX_CELLS or any(abs(b[2] - b[3]) > MAX_RATIO * b[4] for b in bad)

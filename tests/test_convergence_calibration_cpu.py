@@ -1,8 +1,8 @@
 """CPU: the false-alarm rate of the per-epoch draw check, measured on the reference's own draws.
 
 tests/test_gpu_convergence.py holds D device-dropout (or bf16) runs to the reference's R draws at
-every epoch (convergence_stats.draw_bound) and allows at most one epoch-metric cell past the bound,
-none past twice it.  Here every leave-D-out split of the reference's draws plays both roles -- D of
+every epoch (convergence_stats.draw_bound) and allows at most MAX_CELLS epoch-metric cells past the
+bound, none past MAX_RATIO times it.  Here every leave-D-out split of the reference's draws plays both roles -- D of
 them as "device" runs, the other R - D as the reference -- so the rule's false-alarm rate on runs
 that ARE the reference's distribution is measured, not assumed.  (The GPU test compares against
 all R draws, a tighter reference mean than these R - D.)"""
@@ -37,8 +37,8 @@ def test_draw_rule_false_alarm_rate(conv_ref, name):
         bad = CS.violations(te[list(dev)], tr[list(dev)], te[rest], tr[rest], dens)
         cells += len(bad)
         splits += 1
-        fails += int(len(bad) > 1 or any(abs(b[2] - b[3]) > 2.0 * b[4] for b in bad))
+        fails += int(CS.rule_fails(bad))
     print(f"{name}: {splits} splits, {cells} cells past the bound, {fails} splits failing the rule")
-    assert fails / splits <= 0.02, (fails, splits)
+    assert fails / splits <= 0.01, (fails, splits)
     # the reference's draws are not all saturated: the check compares something
     assert (te[:, :, :2].mean(0) < 99.0).any()

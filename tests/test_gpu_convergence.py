@@ -24,6 +24,7 @@ import torch
 import abd_amd
 from abd_amd import training as T
 from abd_amd.models import smallcnn
+import convergence_stats as CS
 from golden_inputs import CONV_CFGS, convergence_data, data_digest
 
 pytestmark = pytest.mark.gpu
@@ -44,15 +45,25 @@ def conv_ref():
     return dict(np.load(p))
 
 
-class DictSet(torch.utils.data.Dataset):
-    def __init__(self, x, y, ind):
-        self.x, self.y, self.ind = x, y, ind
-
-    def __len__(self):
-        return len(self.x)
-
-    def __getitem__(self, i):
-        return {"mfcc": self.x[i], "label": self.y[i], "poison_indicator": self.ind[i]}
+def _dropin_bddataset():
+    """The drop-in prepare_dataset.BDDataset (what the unchanged scripts build, badnets.py:103-104):
+    its loaders take training.train()'s HBM-resident fast path (resident.py)."""
+    import importlib.util
+    import os
+    import sys
+    if "prepare_dataset" in sys.modules:
+        return sys.modules["prepare_dataset"].BDDataset
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-backdoor-attack_amd",
+                     "dropin")
+    sys.path.insert(0, d)   # for its `import _root`
+    try:
+        spec = importlib.util.spec_from_file_location("prepare_dataset", os.path.join(d, "prepare_dataset.py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["prepare_dataset"] = mod
+        spec.loader.exec_module(mod)
+    finally:
+        sys.path.remove(d)
+    return mod.BDDataset
 
 
 def fix_random(seed=35):
@@ -66,7 +77,10 @@ def fix_random(seed=35):
 _DATA = {}
 
 
-def eval_model(name, dev, source, ref, prec="f32"):
+def eval_model(name, dev, source, ref, prec="f32", rng_seed=None):
+    """One eval_model run (badnets.py:127-160).  rng_seed: re-seed torch (CPU batch orders, device
+    dropout) after the data are built -- another draw of the run, as make_convergence.py's
+    SEED_REPLICATES do for the reference."""
     c = CONV_CFGS[name]
     torch.manual_seed(c["init_seed"])
     m = smallcnn(c["K"], c["lf"])
@@ -80,14 +94,17 @@ def eval_model(name, dev, source, ref, prec="f32"):
     d = _DATA[name]
     dg, rdg = data_digest(d), ref[f"{name}_data_digest"]
     assert np.allclose(dg, rdg, rtol=1e-6, atol=0), ("host features differ from the fixture's", dg - rdg)
+    if rng_seed is not None:
+        torch.manual_seed(rng_seed)
     B = c["B"]
+    BDDataset = _dropin_bddataset()
     clean = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(torch.tensor(d["clean_x"]),
                                                                        torch.tensor(d["clean_y"])),
                                         batch_size=B, shuffle=True)
-    bd_train = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bd_x"]), torch.tensor(d["bd_y"]),
-                                                   torch.tensor(d["ind"])), batch_size=B, shuffle=True)
-    bd_test = torch.utils.data.DataLoader(DictSet(torch.tensor(d["bt_x"]), torch.tensor(d["bt_y"]),
-                                                  torch.tensor(d["bt_ind"])), batch_size=B, shuffle=True)
+    bd_train = torch.utils.data.DataLoader(BDDataset(torch.tensor(d["bd_x"]), torch.tensor(d["bd_y"]),
+                                                     torch.tensor(d["ind"])), batch_size=B, shuffle=True)
+    bd_test = torch.utils.data.DataLoader(BDDataset(torch.tensor(d["bt_x"]), torch.tensor(d["bt_y"]),
+                                                    torch.tensor(d["bt_ind"])), batch_size=B, shuffle=True)
     m.set_dropout_source(source)
     tr, te = [], []
     for _ in range(c["epochs"]):
@@ -191,37 +208,92 @@ def final_allowed(conv_ref, name, col, source):
     return max(0.5, spread)
 
 
+# ---------------------------------------------------------------------------------------------
+# Per-epoch clean accuracy / ASR against the reference's run-to-run distribution.
+# A device-dropout run (and a bf16 run: its rounded operands move the trajectory off the reference's
+# within a few epochs) is another DRAW of the attack, not a replay: other masks, other batch orders.
+# make_convergence.py ran the reference's loop under further torch seeds on the same init and data
+# (<name>_test_seeds_ep / _train_seeds_ep); with the fixture run itself that is R reference draws
+# per epoch.  D device runs (other seeds) are averaged and compared at EVERY epoch, for test clean
+# accuracy, test ASR, train accuracy and train ASR, with convergence_stats.draw_bound (K sigma of
+# the difference of the two means).  Many epoch-metric cells are compared per test, so the test
+# allows at most CS.MAX_CELLS (2) cells past the bound and none past CS.MAX_RATIO (2x) it --
+# calibrated on the reference's draws alone (leave-D-out: D of them in place of the device runs, the rest as the reference, every
+# split; tests/test_convergence_calibration_cpu.py).
+D_RUNS = 3
+DEV_SEEDS = (None, 2001, 2002)
+
+
+def check_draws(name, label, runs, conv_ref, d):
+    """runs: list of (tr, te) arrays of the device draws; asserts every epoch and metric."""
+    c = CONV_CFGS[name]
+    dens = {"n_test": c["n_test"], "n_train": c["n_train"], "n_bd": int(d["bt_ind"].sum()),
+            "n_pois": int(d["ind"].sum())}
+    rte, rtr = CS.ref_draws(conv_ref, name)
+    ote, otr = np.stack([te for _, te in runs]), np.stack([tr for tr, _ in runs])
+    refs, ours = {"te": rte, "tr": rtr}, {"te": ote, "tr": otr}
+    unsat = 0
+    print(f"\n{name} [{label}]: per epoch, mean of {len(runs)} draw(s) vs the reference's {rte.shape[0]} draws "
+          "(mean +- sd) and the allowed gap")
+    for what, src, col, den in CS.METRICS:
+        r, o = refs[src][:, :, col], ours[src][:, :, col]
+        bound = CS.draw_bound(r, o.shape[0], dens[den])
+        gap = np.abs(o.mean(0) - r.mean(0))
+        print(f"  {what}:")
+        for e in range(r.shape[1]):
+            unsat += int(r[:, e].mean() < 99.0)
+            flag = "" if gap[e] <= bound[e] else "  <-- outside"
+            print(f"    epoch {e + 1:2d}: ours {o[:, e].mean():7.3f}  ref {r[:, e].mean():7.3f} +- {r[:, e].std(ddof=1):6.3f}"
+                  f"  gap {gap[e]:6.3f} <= {bound[e]:6.3f}{flag}")
+    assert unsat > 0, "no unsaturated epoch compared"
+    bad = CS.violations(ote, otr, rte, rtr, dens)
+    assert not CS.rule_fails(bad), bad
+
+
 @pytest.mark.parametrize("prec", ["f32", "f32split"])
 @pytest.mark.parametrize("name", list(CONV_CFGS))
-def test_device_dropout_final_metrics_within_half_point(dev, conv_ref, name, prec):
-    tr, te, _, _ = eval_model(name, dev, "device", conv_ref, prec)
-    rte = conv_ref[f"{name}_test"]
-    assert tr[-1, 0] < tr[0, 0]                                  # training converges
-    for col in (0, 1):                                           # clean accuracy, ASR (pp)
-        allowed = final_allowed(conv_ref, name, col, "device")
-        assert abs(te[-1, col] - rte[-1, col]) <= allowed, (col, te[-1], rte[-1], allowed)
+def test_device_dropout_epochs_within_reference_draws(dev, conv_ref, name, prec):
+    runs = []
+    for sd in DEV_SEEDS[:D_RUNS]:
+        tr, te, _, d = eval_model(name, dev, "device", conv_ref, prec, rng_seed=sd)
+        assert tr[-1, 0] < tr[0, 0]                              # training converges
+        runs.append((tr, te))
+    check_draws(name, f"{prec}, device dropout", runs, conv_ref, d)
 
 
 # bf16 conv GEMMs (BASELINE configs[2] jingleback and configs[4] flowmur name bf16; badnets shares
-# jingleback's 101 x 40 geometry).  The per-epoch losses of a bf16 run are not expected to track
-# the fp32 reference at 1e-4 (operands rounded to 8 significand bits); the north_star's claim for
-# them is the final clean accuracy / ASR within +-0.5 pp of the reference's -- asserted with the
-# same bound as the fp32 modes (final_allowed: 0.5 pp unless the reference's own spread is wider),
-# in both dropout modes, with the loss gaps printed for DESIGN.md.
+# jingleback's 101 x 40 geometry): per-epoch losses are not expected to track the fp32 reference
+# at 1e-4 (operands rounded to 8 significand bits), so both dropout modes are held to the
+# reference's draw distribution at every epoch (check_draws); the replay with the reference's own
+# masks also prints its gap to the fp32 replay bound (max(0.5 pp, 3x the reference's
+# implementation spread) at that epoch) for DESIGN.md §4.
 BF16_CFGS = [n for n in ("badnets", "jingleback", "flowmur") if n in CONV_CFGS]
 
 
-@pytest.mark.parametrize("source", ["torch_cpu", "device"])
 @pytest.mark.parametrize("name", BF16_CFGS)
-def test_bf16_final_metrics_within_half_point(dev, conv_ref, name, source):
-    tr, te, _, _ = eval_model(name, dev, source, conv_ref, "bf16")
+def test_bf16_replay_epochs(dev, conv_ref, name):
+    tr, te, _, d = eval_model(name, dev, "torch_cpu", conv_ref, "bf16")
     rtr, rte = conv_ref[f"{name}_train"], conv_ref[f"{name}_test"]
+    s_te = conv_ref[f"{name}_test_alt"]
     rel = lambda a, b: np.abs(a - b) / np.maximum(np.abs(b), 1e-12)  # noqa: E731
-    print(f"\n{name} [bf16, {source}] per epoch: |train loss - ref| / ref, clean acc / ASR (GPU vs reference)")
+    n_bd = int(d["bt_ind"].sum())
+    print(f"\n{name} [bf16, reference masks] per epoch: |train loss - ref| / ref; clean acc / ASR GPU vs "
+          "reference, and the fp32 replay bound")
     for e in range(len(rtr)):
-        print(f"  epoch {e + 1:2d}: {rel(tr[e, 0], rtr[e, 0]):.1e}  {te[e, 0]:.3f}/{te[e, 1]:.3f} vs "
-              f"{rte[e, 0]:.3f}/{rte[e, 1]:.3f}")
+        b_acc = max(0.5, 3.0 * abs(s_te[e, 0] - rte[e, 0]), 200.0 / CONV_CFGS[name]["n_test"])
+        b_asr = max(0.5, 3.0 * abs(s_te[e, 1] - rte[e, 1]), 200.0 / n_bd)
+        print(f"  epoch {e + 1:2d}: {rel(tr[e, 0], rtr[e, 0]):.1e}  {te[e, 0]:7.3f}/{te[e, 1]:7.3f} vs "
+              f"{rte[e, 0]:7.3f}/{rte[e, 1]:7.3f}  gaps {abs(te[e, 0] - rte[e, 0]):6.3f} (<= {b_acc:.3f}?) "
+              f"{abs(te[e, 1] - rte[e, 1]):6.3f} (<= {b_asr:.3f}?)")
     assert tr[-1, 0] < tr[0, 0]
-    for col, what in ((0, "clean accuracy (pp)"), (1, "attack success rate (pp)")):
-        allowed = final_allowed(conv_ref, name, col, source)
-        assert abs(te[-1, col] - rte[-1, col]) <= allowed, (what, te[-1], rte[-1], allowed)
+    check_draws(name, "bf16, reference masks", [(tr, te)], conv_ref, d)
+
+
+@pytest.mark.parametrize("name", BF16_CFGS)
+def test_bf16_device_dropout_epochs_within_reference_draws(dev, conv_ref, name):
+    runs = []
+    for sd in DEV_SEEDS[:D_RUNS]:
+        tr, te, _, d = eval_model(name, dev, "device", conv_ref, "bf16", rng_seed=sd)
+        assert tr[-1, 0] < tr[0, 0]
+        runs.append((tr, te))
+    check_draws(name, "bf16, device dropout", runs, conv_ref, d)
