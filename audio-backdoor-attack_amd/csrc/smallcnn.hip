@@ -208,7 +208,7 @@ __device__ __forceinline__ BCoefF bcoef_ff(const BCoef& c) {
 }
 
 // weight repacks: fwd W'[co][t][ci] and dgrad Wd[ci][t][co] (taps flipped via offsets), fc1^T
-constexpr int kGuardTickets = 6;  // BN1, BN2, BN3 guard tickets, a spare, BN2 / BN3 fused finalize (BnFin)
+constexpr int kGuardTickets = 4;  // BN1, BN2, BN3 guard tickets (+ a spare)
 struct PrepArgs {
   const float *c2w, *c3w, *f1w;
   int flat;
@@ -1533,19 +1533,6 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a, int Hx, in
 // of src at output position m shifted by tap t (zero outside the source grid).
 enum { EPI_STORE = 0, EPI_CONV = 1, EPI_FC1 = 2, EPI_DROPGRAD = 3, EPI_PARTIAL = 4 };
 
-// BatchNorm statistics finalized inside the producing conv kernel (conv_ws_spec_kernel, EPI_CONV):
-// the last block to store its partials (arrival ticket) reduces every block's partials and writes
-// what bn_finalize_kernel would -- one launch fewer per BN layer.  ticket == nullptr: not fused.
-struct BnFin {
-  unsigned* ticket;  // zeroed by the step's prep blocks (an earlier launch), re-armed by the last arrival
-  double count;
-  const float* gamma;
-  const float* beta;
-  float* rm;
-  float* rv;
-  float4* coef;
-};
-
 struct NTArgs {
   const float* src;
   int Hs, Ws, Cs;
@@ -1576,7 +1563,6 @@ struct NTArgs {
   // stride splane elements, same NHWC indexing as src)
   const uint16_t* srcs;
   int64_t splane;
-  BnFin fin;      // conv_ws_spec_kernel, EPI_CONV: fused BN finalize (fin.ticket != nullptr)
 };
 
 constexpr int kBM = 128, kKC = 32;
@@ -2675,36 +2661,6 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 // conv_ws_pre_kernel, so results are identical to it.  LDS: 101,376 (weights) + 57,344 / 58,240
 // (4 consumers x 2 buffers x 64 positions x 112 B, + a zero position per buffer in the data
 // gradient) + 256 B.
-// The fused BN finalize (BnFin): wave w reduces channels w, w + nwaves, ... over the nblk partials
-// (lane-strided double sums, then a wave butterfly: a fixed order), lane 0 writes the coefficients
-// and the running statistics exactly as bn_finalize_kernel's thread 0 does.
-__device__ __forceinline__ void bn_finalize_tail(const BnFin& f, const float* __restrict__ part, int nblk, int C) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int c = wave; c < C; c += nw) {
-    double s = 0.0, ss = 0.0;
-    for (int i = lane; i < nblk; i += 64) {
-      s += part[(int64_t)c * nblk + i];
-      ss += part[((int64_t)C + c) * nblk + i];
-    }
-    s = abd::wave_sum_d(s);
-    ss = abd::wave_sum_d(ss);
-    if (lane == 0) {
-      const double mean = s / f.count;
-      double var = ss / f.count - mean * mean;
-      if (var < 0.0) var = 0.0;
-      const float invstd = (float)(1.0 / sqrt(var + (double)kEps));
-      const float alpha = f.gamma[c] * invstd;
-      const float meanf = (float)mean;
-      f.coef[c] = make_float4(meanf, invstd, alpha, f.beta[c] - meanf * alpha);
-      if (f.rm) {
-        const double mo = (double)kMomentum;
-        f.rm[c] = (float)(mo * mean + (1.0 - mo) * (double)f.rm[c]);
-        f.rv[c] = (float)(mo * (var * f.count / (f.count - 1.0)) + (1.0 - mo) * (double)f.rv[c]);
-      }
-    }
-  }
-}
-
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
 #define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
 #endif
@@ -3058,7 +3014,6 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
     a.part[((int64_t)0 * a.N + tid) * a.nblk + blockIdx.x] = s0;
     a.part[((int64_t)1 * a.N + tid) * a.nblk + blockIdx.x] = s1;
   }
-  if (a.fin.ticket != nullptr && last_arrival(a.fin.ticket, gridDim.x)) bn_finalize_tail(a.fin, a.part, a.nblk, N);
 }
 
 struct TNArgs {
@@ -4659,12 +4614,6 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
       a.Bw = w.w2fold;
       a.fold_t = w.ft2;
     }
-    // BN2's finalize fused into the spec kernel's last block (BnFin; its ticket was zeroed by this
-    // step's prep blocks, so only with prep; SyncBN all-reduces the sums between the two instead)
-    const bool fin2 = train && !inst && !sy.on() && prep != nullptr && ws && !bf && planes != 1 &&
-                      ws_kind<EPI_CONV, 3, false>(a) == WS_SPEC;
-    if (fin2)
-      a.fin = BnFin{w.tickets + 4, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1], w.coef + 64};
     if (planes == 1 ? launch_conv_ws_split<EPI_CONV, 1, true>(a, s, abd::PH_CONV2_FWD)
         : ws ? (bf ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV2_FWD)
                    : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV2_FWD))
@@ -4673,11 +4622,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r2, g.H2 * g.W2, 64, P.p[P_BN2W], P.p[P_BN2B],
                                                   inst_coef + B * 64);
-    else if (train && !fin2) {
+    else if (train) {
       if (bn_fwd_finalize(sy, 1, w.part, a.nblk, 64, (double)a.M, P.p[P_BN2W], P.p[P_BN2B], rmu[1], rvu[1],
                           w.coef + 64, nullptr, s))
         return -1;
-    } else if (!train)
+    } else
       bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN2W], P.p[P_BN2B], rm[1], rv[1], 64, w.coef + 64);
     ABD_LAUNCH_CHECK();
     PoolArgs pa = pool_args(g, 2, B);
@@ -4697,10 +4646,6 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     const bool ws3 = (sp3 || bf3) && ws_fits(a);
     a.nblk = !ws3 ? nt_grid_x<32, EPI_CONV>(a) : bf3 ? ws_nblk<EPI_CONV, 1, false>(a) : ws_nblk<EPI_CONV, 3, false>(a);
     a.part = (train && !inst) ? w.part : nullptr;
-    const bool fin3 = train && !inst && !sy.on() && prep != nullptr && ws3 && !bf3 &&
-                      ws_kind<EPI_CONV, 3, false>(a) == WS_SPEC;
-    if (fin3)
-      a.fin = BnFin{w.tickets + 5, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2], w.coef + 128};
     if (ws3 ? (bf3 ? launch_conv_ws_split<EPI_CONV, 1>(a, s, abd::PH_CONV3_FWD)
                    : launch_conv_ws_split<EPI_CONV>(a, s, abd::PH_CONV3_FWD))
             : launch_nt<32, EPI_CONV>(a, s, abd::PH_CONV3_FWD))
@@ -4708,11 +4653,11 @@ int forward(abd_cnn* net, const Work& w, const Params& P, const float* x, int64_
     if (inst)
       inst_coef_kernel<<<(unsigned)B, kT, 0, s>>>(w.r3, g.H3 * g.W3, 32, P.p[P_BN3W], P.p[P_BN3B],
                                                   inst_coef + B * 128);
-    else if (train && !fin3) {
+    else if (train) {
       if (bn_fwd_finalize(sy, 2, w.part, a.nblk, 32, (double)a.M, P.p[P_BN3W], P.p[P_BN3B], rmu[2], rvu[2],
                           w.coef + 128, nullptr, s))
         return -1;
-    } else if (!train)
+    } else
       bn_eval_coef_kernel<<<1, 64, 0, s>>>(P.p[P_BN3W], P.p[P_BN3B], rm[2], rv[2], 32, w.coef + 128);
     ABD_LAUNCH_CHECK();
     if (head) return launch_head(1, *head, s);  // BN3 + pool3 + dropout1 + fc1 partials (fc_head.inc)

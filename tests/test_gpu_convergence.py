@@ -268,6 +268,11 @@ def test_device_dropout_epochs_within_reference_draws(dev, conv_ref, name, prec)
 # masks also prints its gap to the fp32 replay bound (max(0.5 pp, 3x the reference's
 # implementation spread) at that epoch) for DESIGN.md §4.
 BF16_CFGS = [n for n in ("badnets", "jingleback", "flowmur") if n in CONV_CFGS]
+# bf16 replays that hold the fp32 replay bound at every epoch (r5_convergence_tests.txt): asserted.
+# FlowMur's does not -- epoch 1 clean accuracy 0.68 pp (bound 0.50), epoch 4 ASR 2.56 pp (bound 0.64):
+# its clean-label ASR moves between the reference's own fp32 implementations too --
+# and is held to the draw bound only.
+BF16_REPLAY_TIGHT = ("badnets", "jingleback")
 
 
 @pytest.mark.parametrize("name", BF16_CFGS)
@@ -279,12 +284,17 @@ def test_bf16_replay_epochs(dev, conv_ref, name):
     n_bd = int(d["bt_ind"].sum())
     print(f"\n{name} [bf16, reference masks] per epoch: |train loss - ref| / ref; clean acc / ASR GPU vs "
           "reference, and the fp32 replay bound")
+    tight = []
     for e in range(len(rtr)):
         b_acc = max(0.5, 3.0 * abs(s_te[e, 0] - rte[e, 0]), 200.0 / CONV_CFGS[name]["n_test"])
         b_asr = max(0.5, 3.0 * abs(s_te[e, 1] - rte[e, 1]), 200.0 / n_bd)
         print(f"  epoch {e + 1:2d}: {rel(tr[e, 0], rtr[e, 0]):.1e}  {te[e, 0]:7.3f}/{te[e, 1]:7.3f} vs "
               f"{rte[e, 0]:7.3f}/{rte[e, 1]:7.3f}  gaps {abs(te[e, 0] - rte[e, 0]):6.3f} (<= {b_acc:.3f}?) "
               f"{abs(te[e, 1] - rte[e, 1]):6.3f} (<= {b_asr:.3f}?)")
+        if abs(te[e, 0] - rte[e, 0]) > b_acc + 1e-6 or abs(te[e, 1] - rte[e, 1]) > b_asr + 1e-6:  # <= (counts)
+            tight.append(e + 1)
+    if name in BF16_REPLAY_TIGHT:   # the fp32 replay bound at every epoch
+        assert not tight, ("bf16 replay past the fp32 replay bound at epochs", tight)
     assert tr[-1, 0] < tr[0, 0]
     check_draws(name, "bf16, reference masks", [(tr, te)], conv_ref, d)
 
