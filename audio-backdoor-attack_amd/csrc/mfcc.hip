@@ -287,8 +287,9 @@ __global__ void __launch_bounds__(kThreads) row_scale_kernel(const float* __rest
   const int64_t u = blockIdx.x;
   const int64_t row = rows ? rows[u] : u;
   const float* x = wave + row * row_stride;
-  // float4 loads (16-B aligned rows and trigger) with four independent double chains, so a thread
-  // keeps several loads in flight instead of one dependent load + add per element
+  // float4 loads (16-B aligned rows and trigger) with four independent double chains; the loads of
+  // 8 strides are issued before their sums (the loop alone waited on one load per stride: 12 us
+  // for 256 rows of 16,000 samples), the sums keep the per-stride order of the plain loop
   auto sumsq = [&](const float* p, int64_t n) -> double {
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
     const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
@@ -296,7 +297,21 @@ __global__ void __launch_bounds__(kThreads) row_scale_kernel(const float* __rest
     if (al) {
       const float4* p4 = reinterpret_cast<const float4*>(p);
       const int64_t n4 = n / 4;
-      for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+      constexpr int U = 8;
+      int64_t i = threadIdx.x;
+      for (; i + (U - 1) * kThreads < n4; i += U * kThreads) {
+        float4 v[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) v[q] = p4[i + q * kThreads];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          s4[0] += (double)v[q].x * v[q].x;
+          s4[1] += (double)v[q].y * v[q].y;
+          s4[2] += (double)v[q].z * v[q].z;
+          s4[3] += (double)v[q].w * v[q].w;
+        }
+      }
+      for (; i < n4; i += kThreads) {
         const float4 v = p4[i];
         s4[0] += (double)v.x * v.x;
         s4[1] += (double)v.y * v.y;
@@ -1006,15 +1021,19 @@ __device__ __forceinline__ void pair_rows(f2v* pre, const float4* __restrict__ t
     if (r0 + 1 < R) pre[r0 + 1] = f2v{q.z, q.w};
   }
 }
+//   PS: shared-column pairs -- the item's PS FFTs (buffers FS apart) are transformed by the same
+//       threads, butterfly column j of every FFT with ONE set of twiddle / vhat loads (PP == 1)
 template <int M, int R, int NS, int PP, int TWK, bool VMUL, int ZT = R, int RS = R, int PF = kPrefetchRows,
-          bool V4 = false>
+          bool V4 = false, int PS = 1>
 __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2* __restrict__ tws,
                                          const float2* __restrict__ vhats, const float4* __restrict__ t4 = nullptr) {
   static_assert(!(VMUL && TWK != 0), "vhat product and twiddles never share a pass");
   static_assert(!V4 || VMUL, "V4 is the vhat pair table");
+  static_assert(PS == 1 || PP == 1, "shared-column pairs (PS) or distinct pairs (PP), not both");
   constexpr int MR = M / R;
   constexpr int NB = PP * MR;
   constexpr int ROUNDS = (NB + kThreads - 1) / kThreads;
+  constexpr int FS = M + M / 16;  // one padded FFT buffer
   f2v* buf = reinterpret_cast<f2v*>(bufs);
   const f2v* tw = reinterpret_cast<const f2v*>(tws);
   const f2v* vhat = reinterpret_cast<const f2v*>(vhats);
@@ -1043,7 +1062,7 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
     }
   }
   __syncthreads();
-  f2v v[ROUNDS][R];
+  f2v v[ROUNDS][PS][R];
 #pragma unroll
   for (int rd = 0; rd < ROUNDS; ++rd) {
     const int g = min(tid + rd * kThreads, NB - 1);
@@ -1071,22 +1090,27 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
       }
       if constexpr (V4) pair_rows<R, PF, ZT, 0>(pre[rd], t4, j, MR, true);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r >= ZT) {
-          v[rd][r] = f2v{0.0f, 0.0f};
-          continue;
+      for (int q = 0; q < PS; ++q) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r >= ZT) {
+            v[rd][q][r] = f2v{0.0f, 0.0f};
+            continue;
+          }
+          f2v a = buf[q * FS + ((MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR))];
+          if constexpr (VMUL) a = cmul_conj_rt(a, pre[rd][r]);
+          if constexpr (TWK != 0) {
+            if (r > 0) a = cmul_rt(a, pre[rd][r]);
+          }
+          v[rd][q][r] = a;
         }
-        f2v a = buf[(MR % 16 == 0) ? prb + r * (MR + MR / 16) : pidx(rb + r * MR)];
-        if constexpr (VMUL) a = cmul_conj_rt(a, pre[rd][r]);
-        if constexpr (TWK != 0) {
-          if (r > 0) a = cmul_rt(a, pre[rd][r]);
-        }
-        v[rd][r] = a;
+        DftV<R>::run(v[rd][q]);
       }
-      DftV<R>::run(v[rd]);
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[rd][r] = undef_f2v();
+      for (int q = 0; q < PS; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[rd][q][r] = undef_f2v();
     }
   }
   __syncthreads();
@@ -1101,9 +1125,11 @@ __device__ __forceinline__ void spass_pf(float2* __restrict__ bufs, const float2
       const int pd = pidx(dst);
       constexpr bool AFF = (NS == 1) ? (R == 16) : (NS % 16 == 0);
 #pragma unroll
-      for (int r = 0; r < RS; ++r)
-        if (ROUNDS * kThreads == NB || tid + rd * kThreads < NB)
-          buf[AFF ? pd + r * (NS + NS / 16) : pidx(dst + r * NS)] = v[rd][r];
+      for (int q = 0; q < PS; ++q)
+#pragma unroll
+        for (int r = 0; r < RS; ++r)
+          if (ROUNDS * kThreads == NB || tid + rd * kThreads < NB)
+            buf[q * FS + (AFF ? pd + r * (NS + NS / 16) : pidx(dst + r * NS))] = v[rd][q][r];
     }
   }
 }
@@ -1124,17 +1150,21 @@ constexpr int kTw2 = ABD_TW2;
 #else
 constexpr int kTw2 = 4;
 #endif
-template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M, int NO = M>
+// PS > 1 (PP == 1): shared-column pairs, every row's table loads prefetched (the 4-block budget)
+template <int M, int R0, int R1, int R2, int PP, bool VMUL, int NZ = M, int NO = M, int PS = 1>
 __device__ __forceinline__ void fft_plan_pf(float2* buf, const float2* tw, const float2* vhat, const float4* tw4,
                                             const float4* vhat4) {
   static_assert(R0 * R1 * R2 == M, "radix plan must factor M");
   static_assert(NO == M || R2 > 1, "output pruning needs a third pass");
   constexpr int MR0 = M / R0;
   constexpr int ZT0 = (NZ + MR0 - 1) / MR0;
-  spass_pf<M, R0, 1, PP, 0, VMUL, ZT0, R0, kPrefetchRows, VMUL>(buf, nullptr, vhat, vhat4);
-  spass_pf<M, R1, R0, PP, kTw2, false>(buf, tw, nullptr, tw4);
+  constexpr int PF0 = PS > 1 ? R0 : kPrefetchRows, PF1 = PS > 1 ? R1 : kPrefetchRows,
+                PF2 = PS > 1 ? R2 : kPrefetchRows;
+  spass_pf<M, R0, 1, PP, 0, VMUL, ZT0, R0, PF0, VMUL, PS>(buf, nullptr, vhat, vhat4);
+  spass_pf<M, R1, R0, PP, kTw2, false, R1, R1, PF1, false, PS>(buf, tw, nullptr, tw4);
   if constexpr (R2 > 1)
-    spass_pf<M, R2, R0 * R1, PP, kTw3, false, R2, (NO + R0 * R1 - 1) / (R0 * R1)>(buf, tw + R0 * R1, nullptr);
+    spass_pf<M, R2, R0 * R1, PP, kTw3, false, R2, (NO + R0 * R1 - 1) / (R0 * R1), PF2, false, PS>(buf, tw + R0 * R1,
+                                                                                              nullptr);
 }
 
 // Injected sample at signal index s (already clamped into [0, L)); branch-free so the
@@ -1250,13 +1280,16 @@ __device__ __forceinline__ void load_frames(float2* __restrict__ buf, const floa
 // as one (dword-aligned) 16-B load, the chirp as two, the trigger as one -- a quarter of the
 // per-element path's vector-memory instructions, which bound the kernel (TD busy ~85-90 %).
 // Same arithmetic per element as load_frames / fsample.
-template <int M, int NN, int MODE, int NZW>
+// PS > 1: the item's PS consecutive pairs (frames 2(p0+q), 2(p0+q)+1) into buffers FS apart, one
+// chirp load per element group for all of them.
+template <int M, int NN, int MODE, int NZW, int PS = 1>
 __device__ __forceinline__ void load_frames_v4(float2* __restrict__ buf, const float* __restrict__ x, const MfccDev& p,
                                                const InjDev& inj, int p0) {
   static_assert(MODE == ABD_INJECT_NONE || MODE == ABD_INJECT_ADD, "vector gather: no / additive injection");
   static_assert(NZW % 4 == 0, "element groups of 4");
   constexpr int GROUPS = NZW / 4;
   constexpr int ITERS = (GROUPS + kThreads - 1) / kThreads;
+  constexpr int FS = M + M / 16;
   const int hop = p.hop;
   const int base = 2 * p0 * hop - p.pad;  // sample of frame a's element 0
   const int tl = (int)inj.trig_len;
@@ -1266,67 +1299,86 @@ __device__ __forceinline__ void load_frames_v4(float2* __restrict__ buf, const f
     const int gi = ltid() + it * kThreads;
     if (ITERS * kThreads != GROUPS && gi >= GROUPS) break;
     const int n = 4 * gi;
-    float a[4], b[4];
+    float a[PS][4], b[PS][4];
     float2 c[4];
     if (n + 3 < NN) {
-      const int s0 = base + n, s1 = s0 + hop;
-      float4 va, vb;
-      __builtin_memcpy(&va, x + s0, 16);
-      __builtin_memcpy(&vb, x + s1, 16);
       const float4 c01 = ci4[2 * gi], c23 = ci4[2 * gi + 1];
-      a[0] = va.x; a[1] = va.y; a[2] = va.z; a[3] = va.w;
-      b[0] = vb.x; b[1] = vb.y; b[2] = vb.z; b[3] = vb.w;
-      c[0] = make_float2(c01.x, c01.y); c[1] = make_float2(c01.z, c01.w);
-      c[2] = make_float2(c23.x, c23.y); c[3] = make_float2(c23.z, c23.w);
-      if constexpr (MODE == ABD_INJECT_ADD) {
-        // v + t for samples s < tl (fsample): whole groups by one 16-B trigger load each
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int sb = h ? s1 : s0;
-          float* v = h ? b : a;
-          if (sb + 3 < tl) {
-            float4 tv;
-            __builtin_memcpy(&tv, inj.trig + sb, 16);
-            v[0] += tv.x; v[1] += tv.y; v[2] += tv.z; v[3] += tv.w;
-          } else if (sb < tl) {
+      for (int q = 0; q < PS; ++q) {
+        const int s0 = base + 2 * q * hop + n, s1 = s0 + hop;
+        float4 va, vb;
+        __builtin_memcpy(&va, x + s0, 16);
+        __builtin_memcpy(&vb, x + s1, 16);
+        a[q][0] = va.x; a[q][1] = va.y; a[q][2] = va.z; a[q][3] = va.w;
+        b[q][0] = vb.x; b[q][1] = vb.y; b[q][2] = vb.z; b[q][3] = vb.w;
+        if constexpr (MODE == ABD_INJECT_ADD) {
+          // v + t for samples s < tl (fsample): whole groups by one 16-B trigger load each
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (sb + e < tl) v[e] += inj.trig[sb + e];
+          for (int h = 0; h < 2; ++h) {
+            const int sb = h ? s1 : s0;
+            float* v = h ? b[q] : a[q];
+            if (sb + 3 < tl) {
+              float4 tv;
+              __builtin_memcpy(&tv, inj.trig + sb, 16);
+              v[0] += tv.x; v[1] += tv.y; v[2] += tv.z; v[3] += tv.w;
+            } else if (sb < tl) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (sb + e < tl) v[e] += inj.trig[sb + e];
+            }
           }
         }
       }
+      c[0] = make_float2(c01.x, c01.y); c[1] = make_float2(c01.z, c01.w);
+      c[2] = make_float2(c23.x, c23.y); c[3] = make_float2(c23.z, c23.w);
     } else {  // the group straddling NN: per element, zero past the frame
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool ok = n + e < NN;
-        const int s0 = base + min(n + e, NN - 1);
-        a[e] = ok ? fsample<MODE>(x, inj, s0, 0, 0.0f) : 0.0f;
-        b[e] = ok ? fsample<MODE>(x, inj, s0 + hop, 0, 0.0f) : 0.0f;
+#pragma unroll
+        for (int q = 0; q < PS; ++q) {
+          const int s0 = base + 2 * q * hop + min(n + e, NN - 1);
+          a[q][e] = ok ? fsample<MODE>(x, inj, s0, 0, 0.0f) : 0.0f;
+          b[q][e] = ok ? fsample<MODE>(x, inj, s0 + hop, 0, 0.0f) : 0.0f;
+        }
         c[e] = p.chirp_in[min(n + e, NN - 1)];
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f2v zz = cmul_rt(f2v{a[e], b[e]}, f2v{c[e].x, c[e].y});
-      buf[pidx(n + e)] = (n + e < NN) ? make_float2(zz.x, zz.y) : make_float2(0.0f, 0.0f);
-    }
+    for (int q = 0; q < PS; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f2v zz = cmul_rt(f2v{a[q][e], b[q][e]}, f2v{c[e].x, c[e].y});
+        buf[q * FS + pidx(n + e)] = (n + e < NN) ? make_float2(zz.x, zz.y) : make_float2(0.0f, 0.0f);
+      }
   }
 }
 
+// BLUE: the item's PP pairs are shared-column FFTs (spass_pf PS = PP), loaded pair by pair into
+// buffers M + M/16 apart (the vector gather takes all PP at once)
 template <int M, int NN, int PP, bool BLUE, int MODE, int NZW = M>
 __device__ __forceinline__ void load_item(float2* buf, const float* x, const MfccDev& p, const InjDev& inj, int pos,
                                           float rs, int p0, int np) {
   const int first = 2 * p0 * p.hop - p.pad;
   const int last_t = 2 * (p0 + PP) - 1;
   const bool interior = np == PP && first >= 0 && last_t < p.T && last_t * p.hop - p.pad + NN <= (int)p.L;
-  if constexpr (BLUE && PP == 1 && (MODE == ABD_INJECT_NONE || MODE == ABD_INJECT_ADD) && NZW % 4 == 0) {
+  if constexpr (BLUE && (MODE == ABD_INJECT_NONE || MODE == ABD_INJECT_ADD) && NZW % 4 == 0) {
     if (interior && kGatherV4) {
-      load_frames_v4<M, NN, MODE, NZW>(buf, x, p, inj, p0);
+      load_frames_v4<M, NN, MODE, NZW, PP>(buf, x, p, inj, p0);
       return;
     }
   }
-  if (interior) load_frames<M, NN, PP, BLUE, MODE, true, NZW>(buf, x, p, inj, pos, rs, p0, np);
-  else load_frames<M, NN, PP, BLUE, MODE, false, NZW>(buf, x, p, inj, pos, rs, p0, np);
+  if constexpr (BLUE && PP > 1) {
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {  // pairs past the utterance (q >= np) load clamped frames, never stored
+      float2* bq = buf + q * (M + M / 16);
+      if (interior) load_frames<M, NN, 1, BLUE, MODE, true, NZW>(bq, x, p, inj, pos, rs, p0 + q, 1);
+      else load_frames<M, NN, 1, BLUE, MODE, false, NZW>(bq, x, p, inj, pos, rs, p0 + q, 1);
+    }
+  } else {
+    if (interior) load_frames<M, NN, PP, BLUE, MODE, true, NZW>(buf, x, p, inj, pos, rs, p0, np);
+    else load_frames<M, NN, PP, BLUE, MODE, false, NZW>(buf, x, p, inj, pos, rs, p0, np);
+  }
 }
 
 // Persistent blocks walk a contiguous range of (utterance, chunk) work items; each item is
@@ -1359,11 +1411,13 @@ constexpr int kMelSeg = 8;
 #endif
 // float2 slot of a pair's FFT buffer where the segmented mel's partials start (past pidx(nf - 1))
 constexpr int mel_seg_offset(int nf) { return ((nf + nf / 16) + 15) / 16 * 16; }
-template <int M, int NN>
+// PS pairs (buffers FS apart, frames t0 + 2q, t0 + 2q + 1): one chirp / weight load for all of them.
+template <int M, int NN, int PS = 1>
 __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const MfccDev& p, float* __restrict__ db_u,
                                                 int t0) {
   constexpr int NF = NN / 2 + 1;
   constexpr int POFF = ((NN + NN / 16) + 15) / 16 * 16;  // >= pidx(N - 1) + 1
+  constexpr int FS = M + M / 16;
   static_assert(POFF + NF + kMelHP <= M + M / 16, "power array must fit the FFT buffer");
   f2v* buf = reinterpret_cast<f2v*>(bufs);
   f2v* pw = buf + POFF;
@@ -1381,18 +1435,21 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
   for (int rd = 0; rd < PR; ++rd) {
     const int k = ltid() + rd * kThreads;
     if (k < NF + kMelHP) {
-      f2v e = f2v{0.0f, 0.0f};
-      if (k < NF) {
-        const int kn = (k == 0) ? 0 : NN - k;
-        // X[k] = conj(w[k] R[k]) / M  (chirp_out = w / M)
-        f2v P1 = cmul_rt(buf[pidx(k)], cq[rd][0]), Q = cmul_rt(buf[pidx(kn)], cq[rd][1]);
-        P1.y = -P1.y;
-        Q.y = -Q.y;
-        const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
-        const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
-        e = f2v{ar * ar + ai * ai, br * br + bi * bi};
+#pragma unroll
+      for (int q = 0; q < PS; ++q) {
+        f2v e = f2v{0.0f, 0.0f};
+        if (k < NF) {
+          const int kn = (k == 0) ? 0 : NN - k;
+          // X[k] = conj(w[k] R[k]) / M  (chirp_out = w / M)
+          f2v P1 = cmul_rt(buf[q * FS + pidx(k)], cq[rd][0]), Q = cmul_rt(buf[q * FS + pidx(kn)], cq[rd][1]);
+          P1.y = -P1.y;
+          Q.y = -Q.y;
+          const float ar = 0.5f * (P1.x + Q.x), ai = 0.5f * (P1.y - Q.y);
+          const float br = 0.5f * (P1.y + Q.y), bi = 0.5f * (Q.x - P1.x);
+          e = f2v{ar * ar + ai * ai, br * br + bi * bi};
+        }
+        pw[q * FS + k] = e;  // bins NF .. NF + kMelHP - 1: zeros under the slots' padded weights
       }
-      pw[k] = e;  // bins NF .. NF + kMelHP - 1: zeros under the slots' padded weights
     }
   }
   __syncthreads();
@@ -1408,19 +1465,22 @@ __device__ __forceinline__ float power_mel_blue(float2* __restrict__ bufs, const
     w[4 * q + 2] = v.z;
     w[4 * q + 3] = v.w;
   }
-  const f2v* ps = pw + start;
-  f2v s = f2v{0.0f, 0.0f};
-#pragma unroll
-  for (int i = 0; i < kMelHP; ++i) s = fmav(ps[i], f2v{w[i], w[i]}, s);
-  s.x += __shfl_xor(s.x, 1);
-  s.y += __shfl_xor(s.y, 1);
-  const int h = sl & 1;
-  const int t = t0 + h;
   float lmax = -INFINITY;
-  if (t < p.T) {
-    const float d = 10.0f * log10f(fmaxf(h ? s.y : s.x, 1e-10f));
-    db_u[(int64_t)t * p.n_mels + (sl >> 1)] = d;
-    lmax = d;
+#pragma unroll
+  for (int q = 0; q < PS; ++q) {
+    const f2v* ps = pw + q * FS + start;
+    f2v s = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < kMelHP; ++i) s = fmav(ps[i], f2v{w[i], w[i]}, s);
+    s.x += __shfl_xor(s.x, 1);
+    s.y += __shfl_xor(s.y, 1);
+    const int h = sl & 1;
+    const int t = t0 + 2 * q + h;
+    if (t < p.T) {
+      const float d = 10.0f * log10f(fmaxf(h ? s.y : s.x, 1e-10f));
+      db_u[(int64_t)t * p.n_mels + (sl >> 1)] = d;
+      lmax = fmaxf(lmax, d);
+    }
   }
   return lmax;
 }
@@ -1436,7 +1496,10 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
                                                                  float* __restrict__ ws_max,
                                                                  unsigned* __restrict__ queue) {
   // first FFT's first pass reads rows r < ceil(N / (M/R0)) only: the rest is never stored
-  constexpr int kNZW = (BLUE && PP == 1) ? ((NN + M / R0 - 1) / (M / R0)) * (M / R0) : M;
+  constexpr int kNZW = BLUE ? ((NN + M / R0 - 1) / (M / R0)) * (M / R0) : M;
+  // Bluestein: the item's PP pairs are shared-column FFTs (one twiddle / vhat / chirp / mel-weight
+  // load per element for all of them); the other plans map PP pairs onto distinct threads
+  constexpr int PS = BLUE ? PP : 1, PG = BLUE ? 1 : PP;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   constexpr int NTL = 0;
   float2* buf = lds + NTL;
@@ -1456,26 +1519,34 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
   const int P = (p.T + 1) / 2;
   constexpr int nf = NN / 2 + 1;
   const int S = 2 * p.n_mels;
-  // Dynamic item queues (zeroed by the host before the launch): no static split, so blocks
-  // that become resident late cannot leave a tail.  kQueues counters on separate 256-B
-  // lines, each owning a contiguous 1/kQueues of the items; a block pulls from its home
-  // queue, then steals from the others.  Thread 0 grabs the next item while the block
-  // works on the current one.
-  const unsigned qlen = (n_items + kQueues - 1) / kQueues;
+  // Block b's first item is item b (grid <= items); the rest, [gridDim.x, n_items), come from
+  // dynamic queues: no static split, so blocks that become resident late cannot leave a tail.
+  // kQueues counters on separate 256-B lines, each owning a contiguous 1/kQueues of those items; a
+  // block pulls from its home queue, then steals from the others.  Thread 0 grabs the next item
+  // while the block works on the current one.  Block 0 zeroes the counters as it starts (no host
+  // memset launch): no block grabs before it has finished its first item, and a grid of resident
+  // blocks starts within ~1 us (MI355X_MICROARCH.md, workgroup dispatch) while an item takes
+  // >= 10 us.  Were the zeroing ever late it could only hand an item out twice -- both passes write
+  // the same values -- never skip one; block 0 itself is still running after it.
+  const unsigned g0 = gridDim.x;
+  const unsigned rest = n_items > g0 ? n_items - g0 : 0u;
+  const unsigned qlen = (rest + kQueues - 1) / kQueues;
+  if (blockIdx.x == 0 && threadIdx.x < kQueues)
+    __hip_atomic_store(queue + threadIdx.x * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned home = blockIdx.x % kQueues;
   auto grab = [&]() -> unsigned {
     for (int t = 0; t < kQueues; ++t) {
       const unsigned q = (home + t) % kQueues;
       const unsigned v = atomicAdd(queue + q * kQueueStride, 1u);
       const unsigned it = q * qlen + v;
-      if (v < qlen && it < n_items) {
+      if (v < qlen && it < rest) {
         home = q;
-        return it;
+        return g0 + it;
       }
     }
     return ~0u;
   };
-  if (threadIdx.x == 0) s_item = grab();
+  if (threadIdx.x == 0) s_item = blockIdx.x < n_items ? blockIdx.x : ~0u;
   __syncthreads();  // also publishes the staged tables
   unsigned item = s_item;
   while (item != ~0u) {
@@ -1506,13 +1577,13 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
     }
     // no barrier here: the first pass opens with the one that publishes the loaded frames
     if (!(kAblate && (p.ablate & 2))) {
-      fft_plan_pf<M, R0, R1, R2, PP, false, BLUE ? NN : M>(buf, tw, nullptr, p.ftw4, nullptr);
-      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PP, true, M, NN>(buf, tw, p.vhat, p.ftw4, p.vhat4);
+      fft_plan_pf<M, R0, R1, R2, PG, false, BLUE ? NN : M, M, PS>(buf, tw, nullptr, p.ftw4, nullptr);
+      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PG, true, M, NN, PS>(buf, tw, p.vhat, p.ftw4, p.vhat4);
     }
     float lmax = -INFINITY;
-    if constexpr (BLUE && PP == 1) {
+    if constexpr (BLUE) {
       if (p.mel3_w != nullptr && !(kAblate && (p.ablate & 4))) {
-        lmax = power_mel_blue<M, NN>(buf, p, ws_db + (int64_t)u * p.T * p.n_mels, 2 * p0);
+        lmax = power_mel_blue<M, NN, PS>(buf, p, ws_db + (int64_t)u * p.T * p.n_mels, 2 * p0);
         goto item_done;
       }
     }
@@ -1905,6 +1976,14 @@ struct FastPlan {
 #define ABD_BLUE_R1 12
 #endif
 constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (ABD_BLUE_R0 * ABD_BLUE_R1);
+// Bluestein frame pairs per item (shared-column FFTs: one set of table loads for all of them) and
+// the blocks per CU the build is register-budgeted for (PP 2: 39 KB of LDS per block, 4 blocks)
+#ifndef ABD_BLUE_PP
+#define ABD_BLUE_PP 1
+#endif
+#ifndef ABD_BLUE_NBLK
+#define ABD_BLUE_NBLK (ABD_BLUE_PP == 1 ? 8 : 4)
+#endif
 // 2048-point (FlowMur / DABA) and 400-point (BadNets / JingleBack) plans: frame pairs per item and
 // blocks per CU the build is register-budgeted for (measurement builds override them).  Round 5
 // (scripts/stft_plan_ab.sh, feature stage at B = 256, two alternations on one box): 2048 points
@@ -1927,7 +2006,7 @@ constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (AB
 #define ABD_F400_NBLK 4
 #endif
 constexpr int kF400R0 = ABD_F400_R0, kF400R1 = 400 / ABD_F400_R0;
-constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, 1, kBlueR0, kBlueR1},
+constexpr FastPlan kFastPlans[] = {{2304, 1103, 1, ABD_BLUE_PP, kBlueR0, kBlueR1},
                                    {2048, 2048, 0, ABD_F2048_PP, 16, 16},
                                    {400, 400, 0, ABD_F400_PP, kF400R0, kF400R1}};
 
@@ -1973,7 +2052,6 @@ int launch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const i
   if (const char* cap = getenv("ABD_STFT_MAX_BLOCKS")) resident = std::max(1, std::min(resident, atoi(cap)));
   const int64_t items = batch * d.chunks;
   const int grid = (int)std::min<int64_t>(items, (int64_t)resident);
-  ABD_HIP(hipMemsetAsync(queue, 0, kQueues * kQueueStride * sizeof(unsigned), s));
   kern<<<grid, kThreads, lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue);
   ABD_LAUNCH_CHECK();
   return 0;
@@ -1983,8 +2061,8 @@ int dispatch_fast(const MfccDev& d, const float* wave, int64_t row_stride, const
                   const InjDev& ij, const float* rowscale, float* ws_db, float* ws_max, unsigned* queue,
                   hipStream_t s) {
   if (d.M == 2304 && d.N == 1103 && d.bluestein)
-    return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, 1, true>(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max,
-                                                       queue, s);
+    return launch_fast<2304, 1103, kBlueR0, kBlueR1, kBlueR2, ABD_BLUE_PP, true, ABD_BLUE_NBLK>(
+        d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue, s);
   if (d.M == 2048 && d.N == 2048 && !d.bluestein)
     return launch_fast<2048, 2048, 16, 16, 8, ABD_F2048_PP, false, ABD_F2048_NBLK>(d, wave, row_stride, rows, batch, ij,
                                                                                   rowscale, ws_db, ws_max, queue, s);

@@ -331,6 +331,9 @@ def main():
                     "(0 = skip; rank 0 at N = 1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed per-phase profiling steps after warmup")
+    ap.add_argument("--profile-every", type=int, default=4,
+                    help="timed steps: HIP-event brackets on every n-th launch of the dominant kernel(s) only "
+                         "(each bracket serialises the stream, ~4-5 us of idle GPU per event)")
     ap.add_argument("--windows", type=int, default=5, help="equal windows of the timed steps (median reported)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo for 1-GPU rehearsal")
     ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over the global batch")
@@ -400,7 +403,7 @@ def main():
 
     # timed region: exactly `steps` steps between barrier + synchronize; HIP events bracket the
     # dominant kernel(s) on their launch stream, plus one event per window boundary
-    prof = L.PhaseProfiler(live, max_records=len(live) * args.steps + 8)
+    prof = L.PhaseProfiler(live, max_records=len(live) * args.steps + 8, every=max(1, args.profile_every))
     nwin = max(1, min(args.windows, args.steps))
     bounds = [round(i * args.steps / nwin) for i in range(nwin + 1)]
     wev = [torch.cuda.Event(enable_timing=True) for _ in bounds]
@@ -454,6 +457,7 @@ def main():
                     "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes": round(amount * 1e9) if unit == "GB/s" else None,
                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
+                    "sampled_every": max(1, args.profile_every),
                     "formula": ("B*(4L + 4*T*C) / (avg stft_mel + avg db_dct) [SURVEY 8d feature bytes]"
                                 if dominant in FEATURE_PHASES else "per-launch algorithmic FLOP / avg launch")}
             if dominant == "stft_mel" and args.attack == "ultrasonic":

@@ -368,6 +368,10 @@ int abd_adam_f32(float* params, const float* grads, float* exp_avg, float* exp_a
  * 20 conv2 wgrad, 21 conv2 dgrad, ...).  stop() synchronises the recorded events and
  * returns the summed milliseconds and launch counts per phase. */
 int abd_profile_start(unsigned long long phase_mask, int max_records);
+/* The same, bracketing only every `every`-th launch of each enabled phase (1, 1 + every, ...):
+ * each bracket costs the stream a serialising timestamp (~4-5 us of idle GPU on MI355X), so
+ * bench.py samples the launches of its timed steps instead of bracketing all of them. */
+int abd_profile_start_every(unsigned long long phase_mask, int max_records, int every);
 int abd_profile_stop(double* total_ms, int* counts, int n_phases);
 
 #ifdef __cplusplus
