@@ -2662,7 +2662,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 // (4 consumers x 2 buffers x 64 positions x 112 B, + a zero position per buffer in the data
 // gradient) + 256 B.
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
-#define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores
+#define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores, 16 no group barriers (every wave runs free)
 #endif
 #ifndef ABD_SPEC_ILV  // consumer read schedule: 3 (default) A one tap ahead and every step's reads
 #define ABD_SPEC_ILV 3  // two per MFMA gap; 2 one per gap; 1 only B interleaved; 0 all 18 reads at the
@@ -2823,7 +2823,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
         if (cg + 1 < G || tile + 1 < nt) put(stage[c][(cg + 1) & 1], raw[(cg + 1) % 4]);
         if (cg + 1 < G) fetch(p01, cg + 1, need1, raw[(cg + 1) % 4]);
         else fetch(p02, 0, need2, raw[0]);
-        __syncthreads();
+        if constexpr ((ABD_SPEC_ABL & 16) == 0) __syncthreads();
       }
       p01 = p02;
       need1 = need2;
@@ -2969,7 +2969,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
             }
         }
 #endif
-        if (cg + 1 < G) __syncthreads();  // the last group's barrier follows the epilogue
+        if ((ABD_SPEC_ABL & 16) == 0 && cg + 1 < G) __syncthreads();  // the last group's barrier follows the epilogue
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -2989,7 +2989,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orsrc, (int)(ob + 128u * j), 0, 0);
         }
       }
-      __syncthreads();
+      if constexpr ((ABD_SPEC_ABL & 16) == 0) __syncthreads();
     }
     if (EPI == EPI_CONV && a.part != nullptr) {
 #pragma unroll
