@@ -1995,7 +1995,8 @@ constexpr int kBlueR0 = ABD_BLUE_R0, kBlueR1 = ABD_BLUE_R1, kBlueR2 = 2304 / (AB
 // (scripts/stft_plan_ab.sh, feature stage at B = 256, two alternations on one box): 2048 points
 // PP 4 / 1 block-budget 0.0495 ms -> PP 2 / 4 blocks 0.0437 (PP 1: 0.058, PP 3: 0.051); 400 points
 // PP 13 / 1 0.0590 -> PP 8 / 4 0.0504 (PP 6: 0.055, 9: 0.052, 10: 0.054, 17: 0.066; a 20 x 20
-// radix plan at PP 12: 0.058).  Both also take the segmented mel (0.0705 / 0.0576 before it).
+// radix plan at PP 12: 0.058).  Both also take the segmented mel (before it: 400 points 0.0705,
+// 2048 points 0.0576 ms).
 #ifndef ABD_F2048_PP
 #define ABD_F2048_PP 2
 #endif

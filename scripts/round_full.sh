@@ -26,7 +26,10 @@ cat "$O/bench.json"
 cd /tmp && export TMPDIR=/tmp
 CMD="python3 $R/bench.py --steps 10 --warmup 3 --profile-steps 1 --no-cpu --dropin-batches 0"
 step kernel-trace
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt -f csv -- $CMD > "$O/kt.log" 2>&1 || { tail -20 "$O/kt.log"; exit 1; }
+# 60 steps after 20 warmup: the per-kernel averages are steady-state launches, comparable with the
+# bench line's live brackets (10 steps averaged in the cold first launches: stft_mel +10 %)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt -f csv -- \
+  python3 $R/bench.py --steps 60 --warmup 20 --profile-steps 1 --no-cpu --dropin-batches 0 > "$O/kt.log" 2>&1 || { tail -20 "$O/kt.log"; exit 1; }
 [ "${SKIP_PMC:-0}" = 1 ] && exit 0
 step pmc-fetch
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/p_fetch" -o p -f csv -- $CMD > "$O/p_fetch.log" 2>&1 || { tail -20 "$O/p_fetch.log"; exit 1; }
