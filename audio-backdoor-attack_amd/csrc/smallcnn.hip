@@ -441,7 +441,10 @@ __global__ void __launch_bounds__(kT) conv1_bn_pool_kernel(C1Args a) {
 // holds m.  Blocks [0, nprep) repack the weights (prep_weights_body) as in conv1_stats_kernel.
 // forward() caps the chunk grid at the kernel's residency (73 VGPRs: 6 blocks per CU), so the chunks
 // run in one round (a 64-VGPR build for 8 blocks per CU spills and measured the same)
-__global__ void __launch_bounds__(kT) conv1_stats_fold_kernel(C1Args a) {
+#ifndef ABD_C1S_OCC  // waves per SIMD conv1_stats_fold_kernel is register-budgeted for (measurement builds)
+#define ABD_C1S_OCC 1
+#endif
+__global__ void __launch_bounds__(kT, ABD_C1S_OCC) conv1_stats_fold_kernel(C1Args a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   if ((int)blockIdx.x < a.nprep) {
     prep_weights_body(a.prep, blockIdx.x, a.nprep);
@@ -636,8 +639,11 @@ __device__ __forceinline__ void conv1_bwd_stats_body(const C1Args& a) {
 // backward: BN1 dx -> relu mask -> conv1 weight / bias gradient partials (5 per channel).
 // 2 channels per thread (the double-precision BN coefficients would otherwise cap occupancy).
 // FULL (W1 % 3 == 0, every BASELINE geometry): no partial trailing window, branch-free body.
+#ifndef ABD_C1W_OCC  // waves per SIMD conv1_wgrad_kernel is register-budgeted for (measurement builds)
+#define ABD_C1W_OCC 1
+#endif
 template <bool FULL>
-__global__ void __launch_bounds__(kT) conv1_wgrad_kernel(C1Args a) {
+__global__ void __launch_bounds__(kT, ABD_C1W_OCC) conv1_wgrad_kernel(C1Args a) {
   __shared__ __attribute__((aligned(16))) float xs[(kR1 + 1) * 128];
   const int nbh = (a.g.H1 + a.rows - 1) / a.rows;
   const int nchunks = a.B * nbh;
@@ -1472,7 +1478,10 @@ __device__ __forceinline__ void bn_pool_bwd_stats_body(const PoolArgs& a) {
 #define ABD_APPLY_IT 2
 #endif
 constexpr int kApplyIT = ABD_APPLY_IT;
-__global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(PoolArgs a, int Hx, int Wx) {
+#ifndef ABD_BNA_OCC  // waves per SIMD bn_bwd_apply_kernel is register-budgeted for (measurement builds)
+#define ABD_BNA_OCC 1
+#endif
+__global__ void __launch_bounds__(kT, ABD_BNA_OCC) bn_bwd_apply_kernel(PoolArgs a, int Hx, int Wx) {
   const int CG = a.C / 4;
   const int total = a.B * Hx * Wx * CG;
   const int c0 = (threadIdx.x % CG) * 4;  // fixed per thread: kT and the grid stride are multiples of CG
