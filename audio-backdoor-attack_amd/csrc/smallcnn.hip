@@ -2671,7 +2671,8 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 // (4 consumers x 2 buffers x 64 positions x 112 B, + a zero position per buffer in the data
 // gradient) + 256 B.
 #ifndef ABD_SPEC_ABL  // measurement builds (results discarded): 1 no stage writes, 2 no loads,
-#define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores, 16 no group barriers (every wave runs free)
+#define ABD_SPEC_ABL 0  // 4 no MFMAs, 8 no output stores, 16 no group barriers (every wave runs free),
+                        // 32 no B-fragment LDS reads (each register set loaded once)
 #endif
 #ifndef ABD_SPEC_ILV  // consumer read schedule: 3 (default) A one tap ahead and every step's reads
 #define ABD_SPEC_ILV 3  // two per MFMA gap; 2 one per gap; 1 only B interleaved; 0 all 18 reads at the
@@ -2866,12 +2867,22 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
     constexpr int BD = 2, NBV = 4;  // B fragments two steps ahead (as conv_ws_pre_kernel)
     bf16x8 bvs[NBV][NJ][NP];
     auto load_b = [&](int cg, int t, bf16x8 (&bv)[NJ][NP]) {
+      if constexpr ((ABD_SPEC_ABL & 32) != 0) return;  // ablation: B fragments stay in registers
       const int kb = t * CS + cg * 16 + kq;
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + kb]);
     };
+    if constexpr ((ABD_SPEC_ABL & 32) != 0) {  // every B register set loaded once
+#pragma unroll
+      for (int s = 0; s < NBV; ++s)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            bvs[s][j][q] = *reinterpret_cast<const bf16x8*>(&Bs[q][(32 * j + (lane & 31)) * LD + s * CS + kq]);
+    }
 #pragma unroll
     for (int s = 0; s < BD; ++s) load_b(s / 4, s % 4, bvs[s]);
     __syncthreads();  // group 0 staged
