@@ -81,6 +81,32 @@ def test_ultrasonic_b512_inject_gather_every_frame(dev, monkeypatch, max_blocks)
     print(f"ultrasonic B={B} max_blocks={max_blocks}: max rel err {e:.2e}")
 
 
+@pytest.mark.parametrize("max_blocks", [None, 37])
+@pytest.mark.parametrize("fill", ["zero", "ones", "small"])
+def test_stft_queues_any_workspace_contents(dev, monkeypatch, max_blocks, fill):
+    """The persistent STFT's item queues live in the caller's workspace and are zeroed by the
+    kernel's block 0 as it starts (round 5: no host memset launch), each block's first item being its
+    own index.  Whatever the workspace held -- zeros, all-ones counters (every queue looks spent and
+    wraps), small counts (items look taken) -- and when the same workspace is used again, the MFCC is
+    bit-identical to a run on a fresh zeroed workspace."""
+    if max_blocks is not None:
+        monkeypatch.setenv("ABD_STFT_MAX_BLOCKS", str(max_blocks))
+    cfg, w, rows, pois, trig, _ = _ultrasonic_case(13, B=128)
+    wt, rt = torch.tensor(w, device=dev), torch.tensor(rows, device=dev)
+    inj = F.Injection(mode=L.INJECT_ADD, trigger=torch.tensor(trig, device=dev), poison=torch.tensor(pois, device=dev))
+    plan = F.get_plan(cfg, dev)
+    clean = plan.workspace(rows.size).zero_()
+    ref = F.mfcc_batch(wt, cfg, rows=rt, inject=inj, workspace=clean)
+    ws = plan.workspace(rows.size)
+    words = ws[: ws.numel() // 4 * 4].view(torch.int32)
+    words.fill_({"zero": 0, "ones": -1, "small": 3}[fill])
+    got = F.mfcc_batch(wt, cfg, rows=rt, inject=inj, workspace=ws)
+    again = F.mfcc_batch(wt, cfg, rows=rt, inject=inj, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), f"workspace filled {fill}: MFCC differs from the fresh-workspace run"
+    assert torch.equal(again, ref), "a reused workspace changed the MFCC"
+
+
 @pytest.mark.parametrize("max_blocks", [None, 29])
 def test_badnets_b256_400pt_every_frame(dev, monkeypatch, max_blocks):
     """badnets / jingleback front end (400-point radix 16x25 plan, 13 frame pairs per item) with the

@@ -48,6 +48,8 @@ def test_library_rejects_bad_arguments_without_gpu():
         assert lib.abd_smallcnn_create(H, W, 10, 0, C.byref(h)) == 0
         assert lib.abd_smallcnn_flat_features(h) == lf                       # attack_config.txt:11-23
         lib.abd_smallcnn_destroy(h)
+    # sampled profiler brackets (bench.py --profile-every): the period is checked before any HIP call
+    assert lib.abd_profile_start_every(1, 16, 0) == 1001 and lib.abd_profile_start_every(1, -1, 4) == 1001
 
 
 def test_smallcnn_init_and_state_dict_match_reference(golden):
