@@ -188,8 +188,8 @@ def cpu_baseline(batch, threads, n_train=4096, n_test=1024, warmup_steps=5):
             x = tr_w[rows] + pois[rows, None].float() * trig[None]                 # ultrasonic.py:75
             return torch_ref.train_step(model, opt, feat(x), y_eff[rows], pois[rows].long())
         warm = torch.randperm(n_train, generator=g)
-        for k in range(warmup_steps):
-            step(warm[k * batch:(k + 1) * batch])
+        for k in range(warmup_steps):   # wraps around a table smaller than warmup_steps x batch
+            step(warm[(torch.arange(batch) + k * batch) % n_train])
         prep_s = time.perf_counter() - t_prep
         perm = torch.randperm(n_train, generator=g)
         loss, correct, ptot, phit, nb = 0.0, 0, 0, 0, 0
