@@ -22,6 +22,7 @@ EXPORTS = (
     "abd_last_error", "abd_version",
     "abd_mfcc_plan_create", "abd_mfcc_plan_destroy", "abd_mfcc_plan_frames", "abd_mfcc_plan_describe",
     "abd_mfcc_workspace_bytes", "abd_mfcc_f32", "abd_inject_waveform_f32", "abd_inject_workspace_bytes",
+    "abd_inject_row_scales",
     "abd_pydub_overlay_i16", "abd_mfcc_deploy_backward_workspace_bytes", "abd_mfcc_deploy_backward",
     "abd_smallcnn_create", "abd_smallcnn_destroy", "abd_smallcnn_param_count", "abd_smallcnn_param_offsets",
     "abd_smallcnn_flat_features", "abd_smallcnn_workspace_bytes", "abd_smallcnn_workspace_offset", "abd_smallcnn_bn1_folded", "abd_smallcnn_conv2_planes",
@@ -50,6 +51,7 @@ class Inject(C.Structure):
         ("patch_t0", C.c_int), ("patch_t1", C.c_int), ("patch_c0", C.c_int), ("patch_c1", C.c_int),
         ("patch_value", C.c_float),
         ("frames", C.c_void_p), ("frame_pad", C.c_float),
+        ("row_scale", C.c_void_p),
     ]
 
 
@@ -103,6 +105,7 @@ def _declare(lib):
         "abd_mfcc_f32": (i32, [vp, vp, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
         "abd_inject_waveform_f32": (i32, [vp, i64, i64, vp, i64, C.POINTER(Inject), vp, vp, sz, vp]),
         "abd_inject_workspace_bytes": (sz, [i64]),
+        "abd_inject_row_scales": (i32, [vp, i64, i64, i64, C.POINTER(Inject), vp, vp]),
         "abd_pydub_overlay_i16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp]),
         "abd_pydub_overlay_ragged_i16": (i32, [vp, i64, vp, vp, i64, i64, vp, i64, i64, vp, vp, vp]),
         "abd_softmax_entropy": (i32, [vp, i64, i32, vp, vp, vp]),

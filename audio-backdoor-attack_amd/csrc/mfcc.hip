@@ -103,6 +103,7 @@ struct InjDev {
   float pval;
   const int32_t* frames;  // ragged rows: valid frames per row (NULL = all T)
   float fpad;             // value written to frames >= frames[row]
+  bool scale_by_row;      // rowscale is indexed by the table row (abd_inject.row_scale), not the batch row
 };
 
 // Ragged rows (utils/daba_selection_tools.py:70-76: librosa MFCC of a shorter clip, then
@@ -371,7 +372,7 @@ __global__ void __launch_bounds__(kThreads) stft_mel_kernel(MfccDev p, const flo
   const float* x = wave + row * row_stride;
   const bool pois = row_poisoned(inj, u);
   const int pos = (inj.position != nullptr) ? inj.position[u] : 0;
-  const float rs = (rowscale != nullptr) ? rowscale[u] : 0.0f;
+  const float rs = (rowscale != nullptr) ? rowscale[inj.scale_by_row ? row : u] : 0.0f;
 
   const int P = (p.T + 1) / 2;
   const int p0 = c * p.ppb;
@@ -631,7 +632,7 @@ __global__ void __launch_bounds__(kThreads) inject_wave_kernel(const float* __re
   const float* x = wave + row * row_stride;
   const bool pois = row_poisoned(inj, u);
   const int pos = inj.position ? inj.position[u] : 0;
-  const float rs = rowscale ? rowscale[u] : 0.0f;
+  const float rs = rowscale ? rowscale[inj.scale_by_row ? row : u] : 0.0f;
   for (int64_t s = blockIdx.x * (int64_t)kThreads + threadIdx.x; s < L; s += (int64_t)gridDim.x * kThreads)
     out[u * L + s] = inj_sample(x, s, inj, pois, pos, rs);
 }
@@ -1564,7 +1565,7 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
     const float* x = wave + row * row_stride;
     const bool pois = row_poisoned(inj, u);
     const int pos = (inj.position != nullptr) ? inj.position[u] : 0;
-    const float rs = (rowscale != nullptr) ? rowscale[u] : 0.0f;
+    const float rs = (rowscale != nullptr) ? rowscale[inj.scale_by_row ? row : u] : 0.0f;
     const int p0 = c * PP;
     const int np = min(PP, P - p0);
     switch (pois ? inj.mode : ABD_INJECT_NONE) {
@@ -2646,6 +2647,7 @@ static InjDev make_inj(const abd_inject* inj) {
   r.pval = inj->patch_value;
   r.frames = inj->frames;
   r.fpad = inj->frame_pad;
+  r.scale_by_row = false;
   if (r.mode == ABD_INJECT_NONE && r.patch) r.mode = -1;  // patch-only: rows still selected by poison
   return r;
 }
@@ -2659,6 +2661,9 @@ static int check_inj(const InjDev& r) {
   return ABD_OK;
 }
 
+#ifndef ABD_ROW_SCALE_TAB  // measurement builds: 0 ignores abd_inject.row_scale (per-call scales)
+#define ABD_ROW_SCALE_TAB 1
+#endif
 int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_stride, const int32_t* rows,
                  int64_t batch, const abd_inject* inj, float* out, void* workspace, size_t workspace_bytes,
                  abd_stream_t stream) {
@@ -2684,9 +2689,14 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float* rowscale = nullptr;
   if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP) {
-    row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
-    ABD_LAUNCH_CHECK();
-    rowscale = ws_scale;
+    if (ABD_ROW_SCALE_TAB && inj->row_scale != nullptr) {  // the table's scales, computed once (abd_inject_row_scales)
+      rowscale = inj->row_scale;
+      ij.scale_by_row = true;
+    } else {
+      row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, d.L, rows, ij, ws_scale);
+      ABD_LAUNCH_CHECK();
+      rowscale = ws_scale;
+    }
   }
   const int64_t nblk = batch * d.chunks;
   ABD_CHECK(nblk < (1LL << 31), ABD_E_INVALID, "batch too large");
@@ -2733,16 +2743,38 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float* rowscale = nullptr;
   if (ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP) {
-    ABD_CHECK(workspace && workspace_bytes >= abd_inject_workspace_bytes(batch), ABD_E_WORKSPACE,
-              "workspace too small");
-    row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
-                                                                      static_cast<float*>(workspace));
-    ABD_LAUNCH_CHECK();
-    rowscale = static_cast<const float*>(workspace);
+    if (inj->row_scale != nullptr) {
+      rowscale = inj->row_scale;
+      ij.scale_by_row = true;
+    } else {
+      ABD_CHECK(workspace && workspace_bytes >= abd_inject_workspace_bytes(batch), ABD_E_WORKSPACE,
+                "workspace too small");
+      row_scale_kernel<<<dim3((unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
+                                                                        static_cast<float*>(workspace));
+      ABD_LAUNCH_CHECK();
+      rowscale = static_cast<const float*>(workspace);
+    }
   }
   const unsigned gx = (unsigned)std::min<int64_t>((length + kThreads - 1) / kThreads, 64);
   inject_wave_kernel<<<dim3(gx, (unsigned)batch), dim3(kThreads), 0, s>>>(wave, row_stride, length, rows, ij,
                                                                          rowscale, out);
+  ABD_LAUNCH_CHECK();
+  return ABD_OK;
+}
+
+int abd_inject_row_scales(const float* wave, int64_t row_stride, int64_t length, int64_t n_rows,
+                          const abd_inject* inj, float* scales, abd_stream_t stream) {
+  ABD_CHECK(n_rows >= 0 && n_rows < (1LL << 31), ABD_E_INVALID, "n_rows out of range");
+  if (n_rows == 0) return ABD_OK;
+  ABD_CHECK(wave && inj && scales, ABD_E_INVALID, "NULL argument");
+  ABD_CHECK(row_stride >= length && length > 0, ABD_E_INVALID, "row_stride < length");
+  InjDev ij = make_inj(inj);
+  ABD_CHECK(ij.mode == ABD_INJECT_SNR_WINDOW || ij.mode == ABD_INJECT_DEPLOY || ij.mode == ABD_INJECT_DEPLOY_CLAMP,
+            ABD_E_INVALID, "row scales exist for the SNR_WINDOW / DEPLOY modes only (got mode %d)", ij.mode);
+  ij.poison = nullptr;  // every table row (positions are not needed: the scale is the whole clip's)
+  ABD_CHECK(ij.trig != nullptr && ij.trig_len > 0, ABD_E_INVALID, "row scales need a trigger");
+  row_scale_kernel<<<dim3((unsigned)n_rows), dim3(kThreads), 0, static_cast<hipStream_t>(stream)>>>(
+      wave, row_stride, length, nullptr, ij, scales);
   ABD_LAUNCH_CHECK();
   return ABD_OK;
 }

@@ -107,6 +107,7 @@ class Injection:
     patch: tuple | None = None               # (t0, t1, c0, c1, value): BadNets MFCC patch
     frames: torch.Tensor | None = None       # int32 (B,) valid frames per row (ragged clips), None = all
     frame_pad: float = -200.0                # value of the frames past a ragged row's end
+    row_scale: torch.Tensor | None = None    # float32 (N,) per TABLE row (row_scales()), None = per call
 
     def to_c(self) -> L.Inject:
         s = L.Inject()
@@ -131,6 +132,9 @@ class Injection:
             assert self.frames.dtype == torch.int32 and self.frames.is_cuda
             s.frames = self.frames.data_ptr()
             s.frame_pad = float(self.frame_pad)
+        if self.row_scale is not None:
+            assert self.row_scale.dtype == torch.float32 and self.row_scale.is_cuda
+            s.row_scale = self.row_scale.data_ptr()
         return s
 
 
@@ -164,6 +168,19 @@ def mfcc_batch(waves: torch.Tensor, cfg: MfccConfig, rows: torch.Tensor | None =
                              C.byref(inj) if inj is not None else None, out.data_ptr(),
                              ws.data_ptr(), ws.numel(), L.stream_ptr(waves.device))
     L.check(rc, "abd_mfcc_f32")
+    return out
+
+
+def row_scales(waves: torch.Tensor, length: int, inject: Injection) -> torch.Tensor:
+    """The SNR_WINDOW / DEPLOY mixing scale of every row of a resident wave table (flowmur.py:77-80,
+    flowmur_generate_trigger.py:50-52), for ``Injection.row_scale``: the reference mixes each clip
+    once, offline, so a table whose rows and trigger stay fixed needs its scales only once."""
+    L.require_device(waves, "waves")
+    out = torch.empty(waves.shape[0], dtype=torch.float32, device=waves.device)
+    inj = inject.to_c()
+    rc = L.lib().abd_inject_row_scales(waves.data_ptr(), waves.stride(0), length, waves.shape[0], C.byref(inj),
+                                      out.data_ptr(), L.stream_ptr(waves.device))
+    L.check(rc, "abd_inject_row_scales")
     return out
 
 

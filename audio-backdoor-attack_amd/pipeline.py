@@ -206,6 +206,10 @@ class ResidentTrainer:
         else:
             self.position = None
         self._test_pos = {}
+        # the table's SNR / DEPLOY scales, once: rows and trigger are fixed for the whole run (the
+        # reference mixes each clip once, offline), so no step recomputes them
+        self.row_scale = None
+        self._row_scale_key = None
         self.board = None
         self.src_row = None
         if cfg.style is not None:
@@ -290,8 +294,15 @@ class ResidentTrainer:
 
     def _features(self, batch, out):
         rows, _, _, pois, pos = batch
+        if self.cfg.inject_mode in (L.INJECT_SNR_WINDOW, L.INJECT_DEPLOY):
+            key = (self.waves.data_ptr(), self.waves._version, self.trigger.data_ptr(), self.trigger._version)
+            if self.row_scale is None or self._row_scale_key != key:   # recomputed if either is rewritten
+                self.row_scale = F.row_scales(self.waves, self.cfg.length,
+                                              F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger,
+                                                          snr_db=self.cfg.snr_db))
+                self._row_scale_key = key
         inj = F.Injection(mode=self.cfg.inject_mode, trigger=self.trigger, poison=pois, position=pos,
-                          snr_db=self.cfg.snr_db, patch=self.cfg.patch)
+                          snr_db=self.cfg.snr_db, patch=self.cfg.patch, row_scale=self.row_scale)
         F.mfcc_batch(self.waves, self.mcfg, rows=rows, inject=inj, out=out, workspace=self.feat_ws)
 
     def step(self):

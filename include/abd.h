@@ -88,6 +88,11 @@ typedef struct abd_inject {
    * frames are set to frame_pad (-200 there).  NULL = every row has all T frames. */
   const int32_t* frames;
   float frame_pad;
+  /* optional (round 5): the SNR / DEPLOY scale of every row of the wave TABLE, indexed by the
+   * table row (rows[u]), as abd_inject_row_scales() writes it for a resident table whose rows and
+   * trigger do not change (flowmur.py mixes the trigger into each clip once, offline).  NULL = the
+   * call computes the scales of its batch itself (one extra launch per call). */
+  const float* row_scale;
 } abd_inject;
 
 /* wave: row-major utterances (row_stride floats apart, plan length samples each) in
@@ -104,6 +109,12 @@ int abd_inject_waveform_f32(const float* wave, int64_t row_stride, int64_t lengt
                             float* out, void* workspace, size_t workspace_bytes,
                             abd_stream_t stream);
 size_t abd_inject_workspace_bytes(int64_t batch);
+
+/* The SNR_WINDOW / DEPLOY scale of each of n_rows table rows (flowmur.py:77-80,
+ * flowmur_generate_trigger.py:50-52) into scales[n_rows]: every row as if poisoned (inj->poison is
+ * ignored), rows 0..n_rows-1 of the table.  For abd_inject.row_scale. */
+int abd_inject_row_scales(const float* wave, int64_t row_stride, int64_t length, int64_t n_rows,
+                          const abd_inject* inj, float* scales, abd_stream_t stream);
 
 /* FlowMur trigger optimisation, backward half (utils/flowmur_generate_trigger.py:89-104):
  * given dmfcc = d loss / d MFCC (batch, 1, T, n_mfcc) of

@@ -146,6 +146,32 @@ def test_flowmur_b256_2048pt_every_frame(dev, monkeypatch, max_blocks):
     _per_frame_check(got, _oracle(exp, cfg), f"flowmur B=256 max_blocks={max_blocks}")
 
 
+@pytest.mark.parametrize("mode", ["snr", "deploy"])
+def test_row_scale_table_equals_per_call_scales(dev, mode):
+    """Injection.row_scale (abd_inject.row_scale, round 5): the SNR_WINDOW / DEPLOY scales of every
+    table row computed once by abd_inject_row_scales, indexed by the table row, give the same MFCC and
+    the same injected waveforms, bit for bit, as the per-call scales of each batch (rows gathered
+    through a permutation, a poisoned subset)."""
+    cfg = F.MfccConfig.torchaudio(16000, 13, 2048, 512, 16000)
+    w, _ = synth.make_clips_np(320, 16000, 16000, 10, seed=33)
+    r = np.random.default_rng(33)
+    t = torch.tensor(r.uniform(-0.2, 0.2, 8000).astype(np.float32), device=dev)
+    rows = torch.tensor(r.permutation(320)[:256].astype(np.int32), device=dev)
+    pos = torch.tensor(r.integers(0, 8001, 256).astype(np.int32), device=dev)
+    pois = torch.tensor((r.random(256) < 0.3).astype(np.uint8), device=dev)
+    wt = torch.tensor(w, device=dev)
+    m = L.INJECT_SNR_WINDOW if mode == "snr" else L.INJECT_DEPLOY
+    table = F.row_scales(wt, 16000, F.Injection(mode=m, trigger=t, snr_db=30.0))
+    assert table.shape == (320,) and bool(torch.isfinite(table).all()) and bool((table > 0).all())
+    base = dict(mode=m, trigger=t, position=pos, poison=pois, snr_db=30.0)
+    per_call = F.mfcc_batch(wt, cfg, rows=rows, inject=F.Injection(**base))
+    tabled = F.mfcc_batch(wt, cfg, rows=rows, inject=F.Injection(**base, row_scale=table))
+    assert torch.equal(per_call, tabled)
+    wav_call = F.inject_waveform(wt, 16000, F.Injection(**base), rows=rows)
+    wav_tab = F.inject_waveform(wt, 16000, F.Injection(**base, row_scale=table), rows=rows)
+    assert torch.equal(wav_call, wav_tab)
+
+
 def test_daba_b256_slaney_every_frame(dev):
     cfg = F.MfccConfig.librosa(16000, 40, 16000)
     w, _ = synth.make_clips_np(256, 16000, 16000, 10, seed=41)
