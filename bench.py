@@ -7,8 +7,8 @@ gather -> ultrasonic trigger add (10 % poisoned, target 2) -> STFT (n_fft 1103,
 Bluestein) / mel / dB / DCT -> smallcnn forward+backward+CE -> [RCCL all-reduce]
 -> Adam -> device counters.  One "step" = one such batch per GPU.
 
-    python bench.py [--gpus N --steps K --warmup W]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py [--gpus N --steps K --warmup W]       # N > 1: spawns the N ranks itself
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   # WORLD_SIZE must equal N
 
 Rank 0 prints ONE JSON line (value = whole-job utterances/s, max time over ranks).
 """
@@ -317,6 +317,76 @@ def train_flops(H0, W0, K):
     return 3.0 * fwd - c1
 
 
+def rank_envs(n, port, base=None):
+    """Per-rank environments of an N-rank launch on this node (what torch.distributed.run exports)."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        out.append(e)
+    return out
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, cmd, poll_s=0.2):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes (one per GPU, rank r on
+    cuda:r) running `cmd` with the rendezvous environment, wait for all of them and return the first
+    non-zero exit status (0 if every rank succeeded).  Called BEFORE anything touches the GPU -- this
+    process never imports torch -- so each child initialises HIP itself.  Rank 0 writes the JSON
+    line to the inherited stdout; if one rank fails the others are terminated instead of being left
+    waiting in a collective."""
+    import signal
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port())]
+    stopped = []
+
+    def stop(*_):
+        # SIGTERM first; SIGKILL after a grace period (a rank may inherit SIGTERM ignored)
+        if not stopped:
+            stopped.append(time.time())
+        for p in procs:
+            if p.poll() is None:
+                p.terminate() if time.time() - stopped[0] < 5.0 else p.kill()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    try:
+        status = 0
+        while [p.poll() for p in procs].count(None):   # poll every rank (any() would stop at the first)
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                status = status or bad[0]
+                stop()
+            time.sleep(poll_s)
+        for p in procs:
+            p.wait()
+            if p.returncode != 0 and status == 0:
+                status = p.returncode
+        return status if status >= 0 else 128 - status
+    finally:
+        signal.signal(signal.SIGTERM, old)
+
+
+def resolve_world(gpus, environ=None):
+    """(world, spawn): the launch `--gpus N` asks for.  Under a launcher (WORLD_SIZE set) the launcher's
+    world must equal N; without one, N > 1 means this process spawns the N ranks itself."""
+    environ = os.environ if environ is None else environ
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher disagrees with --gpus {gpus}")
+        return gpus, False
+    return gpus, gpus > 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -345,11 +415,13 @@ def main():
                          "bf16: BASELINE configs[2])")
     args = ap.parse_args()
     _PRECISION[0] = args.gemm_precision
+    world, spawn = resolve_world(args.gpus)
+    if spawn:   # no launcher: this process only starts the ranks (it never touches the GPU)
+        sys.exit(spawn_ranks(world, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()

@@ -45,3 +45,19 @@ def test_bench_json_line_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
     assert c["kind"] in ("port", "reference") and c["value"] > 0 and c["cores"] >= 1
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` with no launcher: the parent spawns two ranks itself (here both
+    on the one GPU, gloo), rank 0 prints ONE line with n_gpus 2 / dp2 and the whole-job value."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "8",
+           "--warmup", "2", "--profile-steps", "1", "--no-cpu", "--dropin-batches", "0", "--n-train", "2048"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [ln for ln in res.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 1024
+    assert abs(d["value"] - 1024 * 1e3 / d["ms_per_step"]) <= 1e-3 * d["value"]
+    assert abs(d["value_per_gpu"] - d["value"] / 2) <= 0.1 + 1e-3 * d["value"]
