@@ -29,7 +29,7 @@ EXPORTS = (
     "abd_smallcnn_train_step",
     "abd_smallcnn_apply", "abd_smallcnn_forward", "abd_smallcnn_backward", "abd_smallcnn_eval", "abd_adam_f32",
     "abd_smallcnn_input_grad_workspace_bytes", "abd_smallcnn_input_grad",
-    "abd_profile_start", "abd_profile_start_every", "abd_profile_stop",
+    "abd_profile_start", "abd_profile_start_every", "abd_profile_step", "abd_profile_stop",
 )
 
 # csrc/prof.h phase ids
@@ -143,6 +143,7 @@ def _declare(lib):
         "abd_smallcnn_input_grad": (i32, [vp, vp, i64, vp, vp, vp, f32, vp, vp, vp, vp, sz, vp]),
         "abd_profile_start": (i32, [C.c_ulonglong, i32]),
         "abd_profile_start_every": (i32, [C.c_ulonglong, i32, i32]),
+        "abd_profile_step": (i32, []),
         "abd_profile_stop": (i32, [C.POINTER(C.c_double), C.POINTER(i32), i32]),
     }
     for name, (res, args) in sig.items():
@@ -196,7 +197,8 @@ class PhaseProfiler:
 
     def __init__(self, phases, max_records=4096, every=1):
         """every: bracket only every `every`-th launch of each phase (each bracket serialises the
-        stream: ~4-5 us of idle GPU per event on MI355X)."""
+        stream: ~4-5 us of idle GPU per event on MI355X); once `step()` is called, every launch of
+        the phases inside every `every`-th STEP instead (no aliasing with a phase's launches per step)."""
         self.mask = 0
         for ph in phases:
             self.mask |= 1 << PHASES.index(ph)
@@ -206,6 +208,10 @@ class PhaseProfiler:
     def __enter__(self):
         check(lib().abd_profile_start_every(self.mask, self.max_records, self.every), "abd_profile_start_every")
         return self
+
+    def step(self):
+        """Mark the start of a step (abd_profile_step)."""
+        check(lib().abd_profile_step(), "abd_profile_step")
 
     def __exit__(self, *exc):
         n = len(PHASES)

@@ -1530,16 +1530,22 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
   // dynamic queues: no static split, so blocks that become resident late cannot leave a tail.
   // kQueues counters on separate 256-B lines, each owning a contiguous 1/kQueues of those items; a
   // block pulls from its home queue, then steals from the others.  Thread 0 grabs the next item
-  // while the block works on the current one.  Block 0 zeroes the counters as it starts (no host
-  // memset launch): no block grabs before it has finished its first item, and a grid of resident
-  // blocks starts within ~1 us (MI355X_MICROARCH.md, workgroup dispatch) while an item takes
-  // >= 10 us.  Were the zeroing ever late it could only hand an item out twice -- both passes write
-  // the same values -- never skip one; block 0 itself is still running after it.
+  // in the middle of the current one (after its first FFT: the atomic's latency hides behind the
+  // rest of the item).  Zero counters at launch start (no host memset launch) come from two places:
+  //  * the LAST block to finish resets every counter (and the finish ticket) before it exits, so a
+  //    workspace that already served one launch starts the next at zero, whatever the timing;
+  //  * block 0 zeroes them as it starts, for a workspace that has never served a launch.  That
+  //    store lands within ~1 us of the launch (MI355X_MICROARCH.md, workgroup dispatch) while the
+  //    first grab comes half an item (>= 5 us) in.  Were a grab ever earlier than the store, it
+  //    could only hand an item out twice -- both passes write the same values, every item
+  //    overwrites and never accumulates -- never skip one: block 0 itself is still running after.
   const unsigned g0 = gridDim.x;
   const unsigned rest = n_items > g0 ? n_items - g0 : 0u;
   const unsigned qlen = (rest + kQueues - 1) / kQueues;
-  if (blockIdx.x == 0 && threadIdx.x < kQueues)
-    __hip_atomic_store(queue + threadIdx.x * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned* const finished = queue + kQueueStride / 2;  // second half of queue 0's 256-B line
+  if (blockIdx.x == 0 && threadIdx.x <= kQueues)  // the finish ticket too: no block finishes within 1 us
+    __hip_atomic_store(threadIdx.x < kQueues ? queue + threadIdx.x * kQueueStride : finished, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   unsigned home = blockIdx.x % kQueues;
   auto grab = [&]() -> unsigned {
     for (int t = 0; t < kQueues; ++t) {
@@ -1558,7 +1564,6 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
   unsigned item = s_item;
   while (item != ~0u) {
     unsigned next = 0;
-    if (threadIdx.x == 0) next = grab();
     const int64_t u = item / chunks;
     const int c = (int)(item - u * chunks);
     const int64_t row = rows ? rows[u] : u;
@@ -1583,9 +1588,11 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
       default: load_item<M, NN, PP, BLUE, ABD_INJECT_NONE, kNZW>(buf, x, p, inj, pos, rs, p0, np); break;
     }
     // no barrier here: the first pass opens with the one that publishes the loaded frames
-    if (!(kAblate && (p.ablate & 2))) {
+    if (!(kAblate && (p.ablate & 2)))
       fft_plan_pf<M, R0, R1, R2, PG, false, BLUE ? NN : M, M, PS>(buf, tw, nullptr, p.ftw4, nullptr);
-      if constexpr (BLUE) fft_plan_pf<M, R0, R1, R2, PG, true, M, NN, PS>(buf, tw, p.vhat, p.ftw4, p.vhat4);
+    if (threadIdx.x == 0) next = grab();  // mid-item: see the queue comment above
+    if constexpr (BLUE) {
+      if (!(kAblate && (p.ablate & 2))) fft_plan_pf<M, R0, R1, R2, PG, true, M, NN, PS>(buf, tw, p.vhat, p.ftw4, p.vhat4);
     }
     float lmax = -INFINITY;
     if constexpr (BLUE) {
@@ -1706,6 +1713,16 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
     }
     __syncthreads();  // s_item published; this item's LDS reads are complete
     item = s_item;
+  }
+  // Thread 0 took every grab of this block; its last one returned ~0u before this ticket, so when
+  // the last ticket arrives no block will touch a counter again in this launch: reset them all.
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      for (int q = 0; q < kQueues; ++q)
+        __hip_atomic_store(queue + q * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(finished, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

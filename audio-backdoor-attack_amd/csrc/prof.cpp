@@ -21,12 +21,19 @@ size_t g_next = 0;
 int g_open[64];
 long long g_seen[64];  // begins per phase since start (sampling: every g_every-th is bracketed)
 int g_every = 1;
+// Step-sampled mode (abd_profile_step called at least once since start): a begin is bracketed iff
+// the current step index is a multiple of g_every, so EVERY launch of a phase in a sampled step is
+// timed.  Counting launches instead aliases with the step's launch pattern: a phase launched k
+// times per step with gcd(k, every) > 1 would always bracket the same call site.
+long long g_step = 0;
+bool g_by_step = false;
 }  // namespace
 
 void prof_record(int phase, bool begin, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (begin) {
-    if (g_seen[phase]++ % g_every != 0) {  // not sampled: the matching end records nothing
+    const long long k = g_by_step ? g_step : g_seen[phase]++;
+    if (k % g_every != 0) {  // not sampled: the matching end records nothing
       g_open[phase] = -1;
       return;
     }
@@ -53,6 +60,8 @@ int abd_profile_start_every(unsigned long long phase_mask, int max_records, int 
   if (every < 1 || max_records < 0) return ABD_E_INVALID;
   std::lock_guard<std::mutex> lk(abd::g_mu);
   abd::g_every = every;
+  abd::g_step = 0;
+  abd::g_by_step = false;
   for (int i = 0; i < 64; ++i) abd::g_seen[i] = 0;
   for (auto e : abd::g_pool) (void)hipEventDestroy(e);
   abd::g_pool.clear();
@@ -68,6 +77,13 @@ int abd_profile_start_every(unsigned long long phase_mask, int max_records, int 
     if (rc != hipSuccess) return (int)rc;
   }
   abd::g_prof_mask = phase_mask;
+  return 0;
+}
+
+int abd_profile_step(void) {
+  std::lock_guard<std::mutex> lk(abd::g_mu);
+  if (abd::g_by_step) ++abd::g_step;
+  abd::g_by_step = true;  // the first call marks step 0's start
   return 0;
 }
 

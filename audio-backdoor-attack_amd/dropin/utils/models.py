@@ -15,7 +15,6 @@ from abd_amd.models import smallcnn  # noqa: F401,E402
 from . import reference_module  # noqa: E402
 
 _OTHERS = ("largecnn", "smalllstm", "lstmwithattention", "RNN", "ResNet", "ResidualBlock")
-_ref = reference_module("models")
 
 
 def _missing(name):
@@ -25,5 +24,16 @@ def _missing(name):
     return make
 
 
-for _n in _OTHERS:
-    globals()[_n] = getattr(_ref, _n) if _ref is not None and hasattr(_ref, _n) else _missing(_n)
+def __getattr__(name):
+    """The other backbones resolve lazily (PEP 562): importing this module for smallcnn does not
+    execute the reference's utils/models.py; the first access to one of them does, once."""
+    if name not in _OTHERS:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    ref = reference_module("models")
+    obj = getattr(ref, name) if ref is not None and hasattr(ref, name) else _missing(name)
+    globals()[name] = obj
+    return obj
+
+
+def __dir__():
+    return sorted(set(globals()) | set(_OTHERS))

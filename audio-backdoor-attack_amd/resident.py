@@ -24,6 +24,7 @@ import weakref
 import torch
 from torch.utils.data import DataLoader, Dataset, IterableDataset, TensorDataset
 from torch.utils.data._utils.collate import default_collate
+from torch.utils.data.dataloader import _BaseDataLoaderIter
 
 _CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
@@ -135,6 +136,11 @@ def resident_batches(loader, dev: torch.device, dict_items: bool):
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     if loader.num_workers != 0 or loader.collate_fn is not default_collate or loader.batch_sampler is None:
+        return None
+    # the fast path draws index lists through the iterator's private _next_index(); a torch without
+    # it falls back to iterating the loader (checked on the class: creating an iterator here would
+    # consume the RNG draw the fallback's own iterator makes)
+    if not callable(getattr(_BaseDataLoaderIter, "_next_index", None)):
         return None
     ts = _sources(loader.dataset, dict_items)
     if ts is None:

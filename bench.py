@@ -487,6 +487,7 @@ def main():
     wev[0].record()
     bi = 1
     for k in range(args.steps):
+        prof.step()   # brackets sample whole steps: every launch of the live phases in every n-th step
         tr.step()
         if bi < len(bounds) and k + 1 == bounds[bi]:
             wev[bi].record()
@@ -530,6 +531,9 @@ def main():
                     "algorithmic_bytes": round(amount * 1e9) if unit == "GB/s" else None,
                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
                     "sampled_every": max(1, args.profile_every),
+                    "sampling": "per step (every launch of the live phases in steps 0, n, 2n, ...)",
+                    "launches_per_step": {ph: round(wprof.result.get(ph, (0, 0))[1] / max(args.profile_steps, 1), 3)
+                                          for ph in live},
                     "formula": ("B*(4L + 4*T*C) / (avg stft_mel + avg db_dct) [SURVEY 8d feature bytes]"
                                 if dominant in FEATURE_PHASES else "per-launch algorithmic FLOP / avg launch")}
             if dominant == "stft_mel" and args.attack == "ultrasonic":

@@ -383,6 +383,10 @@ int abd_profile_start(unsigned long long phase_mask, int max_records);
  * each bracket costs the stream a serialising timestamp (~4-5 us of idle GPU on MI355X), so
  * bench.py samples the launches of its timed steps instead of bracketing all of them. */
 int abd_profile_start_every(unsigned long long phase_mask, int max_records, int every);
+/* Mark the start of a step (call once per step, before its launches).  Once called, sampling
+ * is per STEP: every launch of an enabled phase inside steps 0, every, 2 every, ... is bracketed
+ * (launch-count sampling aliases with a phase launched several times per step). */
+int abd_profile_step(void);
 int abd_profile_stop(double* total_ms, int* counts, int n_phases);
 
 #ifdef __cplusplus

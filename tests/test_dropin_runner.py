@@ -97,3 +97,17 @@ def test_runner_resolves_dropin_and_fallthrough(tmp_path):
     pd_file, rt_file, vt_file = r2.stdout.split()
     assert "dropin" in pd_file and "dropin" in rt_file
     assert vt_file == str(tmp_path / "utils" / "visual_tools.py")
+
+
+def test_models_dropin_loads_other_backbones_lazily(tmp_path):
+    """VERDICT r5: `from utils.models import smallcnn` does not execute the reference's utils/models.py;
+    the first access to an out-of-scope backbone does (PEP 562 module __getattr__)."""
+    make_tree(tmp_path)
+    env = dict(os.environ, PYTHONPATH=ROOT, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-c", (
+        "import sys; from abd_amd.run import setup_path; setup_path('attack.py');"
+        "from utils.models import smallcnn; print('utils._reference_models' in sys.modules);"
+        "from utils.models import largecnn; print('utils._reference_models' in sys.modules, largecnn())")],
+        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.split() == ["False", "True", "stand-in", "reference"]

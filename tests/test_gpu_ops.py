@@ -115,3 +115,28 @@ def test_train_step_op_equals_c_abi_step(dev):
 def test_ops_refuse_cpu_tensors():
     with pytest.raises(L.AbdError):
         torch.ops.abd.mfcc(torch.zeros(2, 16000), 16000, 40, 400, 160)
+
+
+def test_profiler_samples_whole_steps(dev):
+    """step-sampled brackets time EVERY launch of a phase inside steps 0, n, 2n, ...
+    (launch-count sampling would bracket only one call site of a phase launched twice per step)."""
+    w, _ = synth.make_clips_np(4, 16000, 16000, 10, seed=6)
+    waves = torch.tensor(w, device=dev)
+    cfg = F.MfccConfig.torchaudio(16000, 40, 400, 160, 16000)
+
+    def run():
+        return F.mfcc_batch(waves, cfg)
+    run()
+    torch.cuda.synchronize()
+    with L.PhaseProfiler(["stft_mel"], max_records=64, every=2) as p:
+        for _ in range(6):          # 6 steps of 2 launches each: steps 0, 2, 4 sampled -> 6 brackets
+            p.step()
+            run()
+            run()
+        torch.cuda.synchronize()
+    assert p.result["stft_mel"][1] == 6
+    with L.PhaseProfiler(["stft_mel"], max_records=64, every=2) as q:   # launch-count mode: 12 / 2
+        for _ in range(12):
+            run()
+        torch.cuda.synchronize()
+    assert q.result["stft_mel"][1] == 6

@@ -84,3 +84,14 @@ def test_cache_key_tracks_in_place_writes():
     k0 = R._key((x, y, i))
     x[0, 0, 0, 0] += 1.0      # e.g. add_trigger_to_mfcc's in-place patch (badnet_trigger.py:25)
     assert R._key((x, y, i)) != k0
+
+
+def test_fast_path_falls_back_without_next_index(monkeypatch):
+    """a torch whose DataLoader iterator lacks _next_index() gets the host loader, not an
+    AttributeError inside train()."""
+    from torch.utils.data.dataloader import _BaseDataLoaderIter
+    from abd_amd import resident
+    ds = torch.utils.data.TensorDataset(torch.zeros(4, 1, 2, 2), torch.zeros(4, dtype=torch.long))
+    loader = torch.utils.data.DataLoader(ds, batch_size=2)
+    monkeypatch.delattr(_BaseDataLoaderIter, "_next_index")
+    assert resident.resident_batches(loader, torch.device("cuda", 0), False) is None
