@@ -30,6 +30,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense ~2.5 PF (no sp
 BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad", "conv2_wgrad", "conv3_wgrad")
 SPLIT_TERMS = 6                 # f32split: six bf16 MFMA terms per fp32-accurate product
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (vector) 157.3 TF
 
 
 def algorithmic_work(phase, B, H0, W0, K, n_mels, T, C, L):
@@ -562,6 +563,16 @@ def main():
             tb, tsrc = load_traffic(ph) if headline else (None, None)
             per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "peak": pk, "frac": round(ach / pk, 4),
                               "ms": round(pms / pcnt, 4), "traffic": tb, "traffic_source": tsrc}
+            if ph == "stft_mel" and cfg.n_fft == 1103:
+                # the limiter the byte model misses: the Bluestein FFTs' arithmetic
+                # (5 M log2 M per complex M-point FFT, two per frame pair) against the fp32 VECTOR
+                # peak (MI355X_MICROARCH.md: 157.3 TF, 256 CUs x 4 SIMD-32 x FMA at 2.4 GHz)
+                tf = stft_flops(args.batch, T) / (pms / pcnt / 1e3) / 1e12
+                per_kernel["stft_mel_valu"] = {"bound": "valu", "achieved": round(tf, 2), "unit": "TFLOP/s",
+                                               "peak": FP32_VECTOR_PEAK_TFLOPS,
+                                               "frac": round(tf / FP32_VECTOR_PEAK_TFLOPS, 4),
+                                               "ms": round(pms / pcnt, 4),
+                                               "formula": "B * ceil(T/2) pairs * 2 FFTs * 5 M log2 M, M = 2304"}
         cpu = None
         if world == 1 and not args.no_cpu and args.cpu_train > 0 and args.attack == "ultrasonic":
             cpu = cpu_baseline(args.batch, cpu_threads(), n_train=args.cpu_train)

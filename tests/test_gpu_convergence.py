@@ -220,8 +220,17 @@ def final_allowed(conv_ref, name, col, source):
 # allows at most CS.MAX_CELLS (2) cells past the bound and none past CS.MAX_RATIO (2x) it --
 # calibrated on the reference's draws alone (leave-D-out: D of them in place of the device runs, the rest as the reference, every
 # split; tests/test_convergence_calibration_cpu.py).
-D_RUNS = 3
-DEV_SEEDS = (None, 2001, 2002)
+# Device draws per config: 8, and 48 for FlowMur, whose clean-label ASR is the noisiest metric
+# (sd up to 6.5 pp per draw; the reference side has 41 draws of it, make_convergence.py
+# SEED_REPLICATES, and its K is 3.5: convergence_stats.K_BY_CFG) -- so its test-ASR bound is <= 5 pp at
+# every epoch and a 4-5 pp shift is caught (test_convergence_calibration_cpu.py).
+D_RUNS = {"flowmur": 48}
+D_DEFAULT = 8
+DEV_SEEDS = (None,) + tuple(range(2001, 2060))
+
+
+def n_draws(name):
+    return D_RUNS.get(name, D_DEFAULT)
 
 
 def check_draws(name, label, runs, conv_ref, d):
@@ -246,15 +255,23 @@ def check_draws(name, label, runs, conv_ref, d):
             print(f"    epoch {e + 1:2d}: ours {o[:, e].mean():7.3f}  ref {r[:, e].mean():7.3f} +- {r[:, e].std(ddof=1):6.3f}"
                   f"  gap {gap[e]:6.3f} <= {bound[e]:6.3f}{flag}")
     assert unsat > 0, "no unsaturated epoch compared"
-    bad = CS.violations(ote, otr, rte, rtr, dens)
+    bad = CS.violations(ote, otr, rte, rtr, dens, k_sigma=CS.k_sigma(name, len(runs)))
     assert not CS.rule_fails(bad), bad
+    # final epoch: the mean of the draws' final clean accuracy / ASR against the
+    # reference's own final, within final_allowed's device bound -- max(0.5 pp, the reference's
+    # implementation spread, the range of its own RNG replicates)
+    for col, what in ((0, "clean acc"), (1, "ASR")):
+        allowed = final_allowed(conv_ref, name, col, "device")
+        got, ref = float(ote[:, -1, col].mean()), float(conv_ref[f"{name}_test"][-1, col])
+        print(f"  final {what}: mean of draws {got:.3f} vs reference {ref:.3f} (allowed {allowed:.3f})")
+        assert abs(got - ref) <= allowed, (what, got, ref, allowed)
 
 
 @pytest.mark.parametrize("prec", ["f32", "f32split"])
 @pytest.mark.parametrize("name", list(CONV_CFGS))
 def test_device_dropout_epochs_within_reference_draws(dev, conv_ref, name, prec):
     runs = []
-    for sd in DEV_SEEDS[:D_RUNS]:
+    for sd in DEV_SEEDS[:n_draws(name)]:
         tr, te, _, d = eval_model(name, dev, "device", conv_ref, prec, rng_seed=sd)
         assert tr[-1, 0] < tr[0, 0]                              # training converges
         runs.append((tr, te))
@@ -268,11 +285,31 @@ def test_device_dropout_epochs_within_reference_draws(dev, conv_ref, name, prec)
 # masks also prints its gap to the fp32 replay bound (max(0.5 pp, 3x the reference's
 # implementation spread) at that epoch) for DESIGN.md §4.
 BF16_CFGS = [n for n in ("badnets", "jingleback", "flowmur") if n in CONV_CFGS]
-# bf16 replays that hold the fp32 replay bound at every epoch (r5_convergence_tests.txt): asserted.
-# FlowMur's does not -- epoch 1 clean accuracy 0.68 pp (bound 0.50), epoch 4 ASR 2.56 pp (bound 0.64):
-# its clean-label ASR moves between the reference's own fp32 implementations too --
-# and is held to the draw bound only.
-BF16_REPLAY_TIGHT = ("badnets", "jingleback")
+# The bf16 replay is held to the fp32 replay bound at every epoch.  FlowMur's misses it (round 5:
+# epoch 1 clean accuracy 0.68 pp against 0.50, epoch 4 ASR 2.56 pp against 0.64; its clean-label ASR
+# moves between the reference's own fp32 implementations too): an OPEN known
+# limitation, tracked as a non-strict xfail so the suite reports it every run (XPASS if it closes),
+# beside the draw bound it does meet.
+BF16_REPLAY_OPEN = ("flowmur",)
+
+
+@pytest.mark.parametrize("name", [pytest.param(n, marks=pytest.mark.xfail(
+    reason="known limitation: FlowMur bf16 replay past the fp32 replay bound (DESIGN.md §4)", strict=False))
+    if n in BF16_REPLAY_OPEN else n for n in BF16_CFGS])
+def test_bf16_replay_fp32_bound(dev, conv_ref, name):
+    """bf16 with the reference's own masks: clean accuracy / ASR within the fp32 replay bound
+    (max(0.5 pp, 3x the reference's implementation spread, two samples)) at EVERY epoch."""
+    tr, te, _, d = eval_model(name, dev, "torch_cpu", conv_ref, "bf16")
+    rte, s_te = conv_ref[f"{name}_test"], conv_ref[f"{name}_test_alt"]
+    n_bd = int(d["bt_ind"].sum())
+    tight = []
+    for e in range(len(rte)):
+        b_acc = max(0.5, 3.0 * abs(s_te[e, 0] - rte[e, 0]), 200.0 / CONV_CFGS[name]["n_test"])
+        b_asr = max(0.5, 3.0 * abs(s_te[e, 1] - rte[e, 1]), 200.0 / n_bd)
+        if abs(te[e, 0] - rte[e, 0]) > b_acc + 1e-6 or abs(te[e, 1] - rte[e, 1]) > b_asr + 1e-6:  # <= (counts)
+            tight.append((e + 1, round(abs(te[e, 0] - rte[e, 0]), 3), round(b_acc, 3),
+                          round(abs(te[e, 1] - rte[e, 1]), 3), round(b_asr, 3)))
+    assert not tight, ("bf16 replay past the fp32 replay bound (epoch, acc gap, bound, ASR gap, bound)", tight)
 
 
 @pytest.mark.parametrize("name", BF16_CFGS)
@@ -293,8 +330,7 @@ def test_bf16_replay_epochs(dev, conv_ref, name):
               f"{abs(te[e, 1] - rte[e, 1]):6.3f} (<= {b_asr:.3f}?)")
         if abs(te[e, 0] - rte[e, 0]) > b_acc + 1e-6 or abs(te[e, 1] - rte[e, 1]) > b_asr + 1e-6:  # <= (counts)
             tight.append(e + 1)
-    if name in BF16_REPLAY_TIGHT:   # the fp32 replay bound at every epoch
-        assert not tight, ("bf16 replay past the fp32 replay bound at epochs", tight)
+    print(f"  epochs past the fp32 replay bound: {tight} (test_bf16_replay_fp32_bound)")
     assert tr[-1, 0] < tr[0, 0]
     check_draws(name, "bf16, reference masks", [(tr, te)], conv_ref, d)
 
@@ -302,7 +338,7 @@ def test_bf16_replay_epochs(dev, conv_ref, name):
 @pytest.mark.parametrize("name", BF16_CFGS)
 def test_bf16_device_dropout_epochs_within_reference_draws(dev, conv_ref, name):
     runs = []
-    for sd in DEV_SEEDS[:D_RUNS]:
+    for sd in DEV_SEEDS[:n_draws(name)]:
         tr, te, _, d = eval_model(name, dev, "device", conv_ref, "bf16", rng_seed=sd)
         assert tr[-1, 0] < tr[0, 0]
         runs.append((tr, te))
