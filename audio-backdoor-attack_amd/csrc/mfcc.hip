@@ -1308,7 +1308,17 @@ __device__ __forceinline__ void load_frames_v4(float2* __restrict__ buf, const f
     const int n = 4 * gi;
     float a[PS][4], b[PS][4];
     float2 c[4];
-    if (n + 3 < NN) {
+    if (kAblate && (p.ablate & 1)) {  // measurement builds: no sample / trigger / chirp loads
+#pragma unroll
+      for (int q = 0; q < PS; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[q][e] = (float)(n + e);
+          b[q][e] = (float)(p0 + q);
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) c[e] = make_float2(1.0f, (float)e);
+    } else if (n + 3 < NN) {
       const float4 c01 = ci4[2 * gi], c23 = ci4[2 * gi + 1];
 #pragma unroll
       for (int q = 0; q < PS; ++q) {
@@ -2720,7 +2730,14 @@ int abd_mfcc_f32(const abd_mfcc_plan* plan, const float* wave, int64_t row_strid
   const size_t lds = 2 * (size_t)d.ppb * d.M * sizeof(float2);
   abd::prof_begin(abd::PH_STFT_MEL, s);
   if (d.fast) {
-    if (dispatch_fast(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue, s) != 0) return -1;
+    if constexpr (kAblate) {  // measurement builds only: ABD_STFT_ABLATE bits (MfccDev::ablate) per launch
+      MfccDev da = d;
+      const char* e = getenv("ABD_STFT_ABLATE");
+      da.ablate = e ? atoi(e) : 0;
+      if (dispatch_fast(da, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue, s) != 0) return -1;
+    } else if (dispatch_fast(d, wave, row_stride, rows, batch, ij, rowscale, ws_db, ws_max, queue, s) != 0) {
+      return -1;
+    }
   } else {
     stft_mel_kernel<<<dim3((unsigned)nblk), dim3(kThreads), lds, s>>>(d, wave, row_stride, rows, batch, ij, rowscale,
                                                                     ws_db, ws_max);
