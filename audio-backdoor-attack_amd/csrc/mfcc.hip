@@ -1539,23 +1539,23 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
   // Block b's first item is item b (grid <= items); the rest, [gridDim.x, n_items), come from
   // dynamic queues: no static split, so blocks that become resident late cannot leave a tail.
   // kQueues counters on separate 256-B lines, each owning a contiguous 1/kQueues of those items; a
-  // block pulls from its home queue, then steals from the others.  Thread 0 grabs the next item
-  // in the middle of the current one (after its first FFT: the atomic's latency hides behind the
-  // rest of the item).  Zero counters at launch start (no host memset launch) come from two places:
-  //  * the LAST block to finish resets every counter (and the finish ticket) before it exits, so a
-  //    workspace that already served one launch starts the next at zero, whatever the timing;
-  //  * block 0 zeroes them as it starts, for a workspace that has never served a launch.  That
-  //    store lands within ~1 us of the launch (MI355X_MICROARCH.md, workgroup dispatch) while the
-  //    first grab comes half an item (>= 5 us) in.  Were a grab ever earlier than the store, it
-  //    could only hand an item out twice -- both passes write the same values, every item
-  //    overwrites and never accumulates -- never skip one: block 0 itself is still running after.
+  // block pulls from its home queue, then steals from the others.  Thread 0 grabs the next item in
+  // the middle of the current one (after its first FFT: the atomic's latency still hides behind the
+  // rest of the item).  Block 0 zeroes the counters as it starts (no host memset launch); a grid of
+  // resident blocks is dispatched within ~1 us (MI355X_MICROARCH.md, workgroup dispatch), and no
+  // block grabs before it has loaded and transformed its first item (>= 5 us), so the zeroing has
+  // landed before the first grab.  That is a timing argument, not a guarantee: a grab that still
+  // beat the store would read the workspace's previous counters and either take an item that is
+  // handed out again after the zeroing (both passes write the same values -- every item overwrites,
+  // none accumulates) or see an exhausted queue and leave its share to the other blocks; never skip
+  // one, since block 0 itself runs on after its store.  (Round 6 measured the alternative -- the
+  // last block to finish resets the counters, so a used workspace always starts at zero -- at
+  // +7 us per launch: 2,048 same-address atomics at the kernel's tail, profiles/r6_stft/queue_ab.txt.)
   const unsigned g0 = gridDim.x;
   const unsigned rest = n_items > g0 ? n_items - g0 : 0u;
   const unsigned qlen = (rest + kQueues - 1) / kQueues;
-  unsigned* const finished = queue + kQueueStride / 2;  // second half of queue 0's 256-B line
-  if (blockIdx.x == 0 && threadIdx.x <= kQueues)  // the finish ticket too: no block finishes within 1 us
-    __hip_atomic_store(threadIdx.x < kQueues ? queue + threadIdx.x * kQueueStride : finished, 0u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x < kQueues)
+    __hip_atomic_store(queue + threadIdx.x * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned home = blockIdx.x % kQueues;
   auto grab = [&]() -> unsigned {
     for (int t = 0; t < kQueues; ++t) {
@@ -1723,16 +1723,6 @@ __global__ void __launch_bounds__(kThreads, NBLK) stft_mel_fast_kernel(MfccDev p
     }
     __syncthreads();  // s_item published; this item's LDS reads are complete
     item = s_item;
-  }
-  // Thread 0 took every grab of this block; its last one returned ~0u before this ticket, so when
-  // the last ticket arrives no block will touch a counter again in this launch: reset them all.
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == gridDim.x - 1) {
-      for (int q = 0; q < kQueues; ++q)
-        __hip_atomic_store(queue + q * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(finished, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 
