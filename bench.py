@@ -337,16 +337,31 @@ def free_port():
         return s.getsockname()[1]
 
 
+def _relay(stream, rank):
+    """Forward a rank's stdout: rank 0's JSON line(s) to this process's stdout, every other line
+    (collective libraries print connection banners to stdout) to stderr."""
+    for raw in iter(stream.readline, b""):
+        line = raw.decode(errors="replace")
+        out = sys.stdout if rank == 0 and line.lstrip().startswith("{") else sys.stderr
+        out.write(line)
+        out.flush()
+    stream.close()
+
+
 def spawn_ranks(n, cmd, poll_s=0.2):
     """`bench.py --gpus N` without a launcher: start N fresh child processes (one per GPU, rank r on
     cuda:r) running `cmd` with the rendezvous environment, wait for all of them and return the first
     non-zero exit status (0 if every rank succeeded).  Called BEFORE anything touches the GPU -- this
-    process never imports torch -- so each child initialises HIP itself.  Rank 0 writes the JSON
-    line to the inherited stdout; if one rank fails the others are terminated instead of being left
-    waiting in a collective."""
+    process never imports torch -- so each child initialises HIP itself.  Rank 0's JSON line is
+    relayed to stdout, everything else the ranks print goes to stderr; if one rank fails the others
+    are terminated instead of being left waiting in a collective."""
     import signal
     import subprocess
-    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port())]
+    import threading
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE) for e in rank_envs(n, free_port())]
+    relays = [threading.Thread(target=_relay, args=(p.stdout, r), daemon=True) for r, p in enumerate(procs)]
+    for t in relays:
+        t.start()
     stopped = []
 
     def stop(*_):
@@ -369,6 +384,8 @@ def spawn_ranks(n, cmd, poll_s=0.2):
             p.wait()
             if p.returncode != 0 and status == 0:
                 status = p.returncode
+        for t in relays:
+            t.join(timeout=10.0)
         return status if status >= 0 else 128 - status
     finally:
         signal.signal(signal.SIGTERM, old)

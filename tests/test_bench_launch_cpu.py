@@ -59,3 +59,14 @@ def test_bench_rejects_world_size_mismatch():
                          capture_output=True, text=True, timeout=60)
     assert res.returncode != 0
     assert "disagrees with --gpus 2" in res.stderr
+
+
+def test_spawn_ranks_relays_only_rank0_json(capfd):
+    """Collective libraries print banners to stdout (gloo: "[Gloo] Rank 0 is connected to ..."): only
+    rank 0's JSON line reaches stdout, the rest goes to stderr."""
+    code = ("import os, sys; r = os.environ['RANK']; print('[Gloo] Rank ' + r + ' is connected'); "
+            "print('{\"rank\": ' + r + '}') if r == '0' else print('{\"rank\": 9}'); sys.stdout.flush()")
+    assert bench.spawn_ranks(2, [sys.executable, "-c", code], poll_s=0.01) == 0
+    out, err = capfd.readouterr()
+    assert out.strip().splitlines() == ['{"rank": 0}'], out
+    assert "[Gloo] Rank 0" in err and "[Gloo] Rank 1" in err and '{"rank": 9}' in err
