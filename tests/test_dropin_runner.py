@@ -111,3 +111,29 @@ def test_models_dropin_loads_other_backbones_lazily(tmp_path):
         cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.split() == ["False", "True", "stand-in", "reference"]
+
+
+def test_runner_config_yaml_sets_argparse_defaults(tmp_path):
+    """`abd_amd.run --config config/x.yaml script.py`: YAML keys become the script's argparse
+    defaults (typed: load_clean_data False stays False), command-line flags win, num_epoches ->
+    num_epochs, unknown keys are reported and ignored."""
+    (tmp_path / "attack.py").write_text(
+        "import argparse, json, sys\n"
+        "p = argparse.ArgumentParser()\n"
+        "p.add_argument('--model', type=str, default='largecnn')\n"
+        "p.add_argument('--load_clean_data', type=bool, default=True)\n"
+        "p.add_argument('--n_fft', type=int, default=400)\n"
+        "p.add_argument('--num_epochs', type=int, default=300)\n"
+        "p.add_argument('--learning_rate', type=float, default=0.001)\n"
+        "a = p.parse_args()\n"
+        "json.dump(vars(a), open(sys.argv[0] + '.json', 'w'))\n")
+    (tmp_path / "cfg.yaml").write_text("model: smallcnn\nload_clean_data: False\nn_fft: 1103\nnum_epoches: 7\n"
+                                       "learning_rate: 0.0001\ntrigger_pos: mid\n")
+    env = dict(os.environ, PYTHONPATH=ROOT, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-m", "abd_amd.run", "--config", "cfg.yaml", "attack.py", "--n_fft", "2048"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads((tmp_path / "attack.py.json").read_text())
+    assert got == {"model": "smallcnn", "load_clean_data": False, "n_fft": 2048, "num_epochs": 7,
+                   "learning_rate": 0.0001}, got
+    assert "trigger_pos" in r.stderr
