@@ -1,0 +1,4 @@
+# Round 6: STFT queue tags -- stft_mel A/B (HEAD library as libabd_old.so vs the working tree) + the MFCC GPU tests
+mkdir -p gpurun_out/r6_qtag
+for v in _old "" _old "" _old ""; do echo "lib$v"; ABD_LIB=$PWD/audio-backdoor-attack_amd/libabd$v.so BITS=0,0 timeout -k 10 120 python scripts/stft_ablate_time.py || exit 1; done > gpurun_out/r6_qtag/ab.txt 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_mfcc_scale.py tests/test_gpu_mfcc.py tests/test_gpu_flowmur.py > gpurun_out/r6_qtag/tests.txt 2>&1
