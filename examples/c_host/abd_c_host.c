@@ -47,6 +47,7 @@ static void* read_file(const char* dir, const char* name, size_t bytes) {
   FILE* f = fopen(path, "rb");
   if (!f) die("open", path);
   void* p = malloc(bytes ? bytes : 1);
+  if (!p) die("out of host memory", path);
   if (fread(p, 1, bytes, f) != bytes) die("short read", path);
   fclose(f);
   return p;
@@ -70,6 +71,7 @@ static void* to_device(const void* h, size_t bytes) {
 
 static void to_file(const char* dir, const char* name, const void* d, size_t bytes) {
   void* h = malloc(bytes ? bytes : 1);
+  if (!h) die("out of host memory", name);
   HIPCHK(hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
   write_file(dir, name, h, bytes);
   free(h);
@@ -83,7 +85,7 @@ int main(int argc, char** argv) {
   const char* dir = argv[1];
   const int64_t B = atoll(argv[2]);
   const int K = atoi(argv[3]);
-  if (B < 1 || K < 2) die("arguments", "B >= 1 and K >= 2 required");
+  if (B < 1 || B > (1 << 20) || K < 2) die("arguments", "B >= 1 and K >= 2 required (B <= 2^20)");
   hipStream_t stream;
   HIPCHK(hipStreamCreate(&stream));
 
