@@ -2681,9 +2681,17 @@ __global__ void __launch_bounds__(512, 1) conv_ws_pre_kernel(NTArgs a) {
 #ifndef ABD_WS_SPEC  // conv_ws_spec_kernel replaces conv_ws_pre_kernel: 2 everywhere, 1 the forwards
 #define ABD_WS_SPEC 2  // only, 0 nowhere (measurement builds)
 #endif
-template <int EPI, int NJ = 2>
+// NP = 1 (bf16 mode, conv2): the A source is the producer layer's bf16 plane (NTArgs::srcs), loaded 16 B
+// per unit and stored to the stage unchanged (no split); one MFMA term per step.  Same tiles, K order
+// and products as conv_ws_dma_kernel<EPI, 1, 2, true>, whose LDS-DMA pieces stalled the issuing
+// waves' MFMAs (r6_bf16abl: without the DMA issue the bf16 forward ran 39 -> 21 us at B = 256).
+#ifndef ABD_BF16_SPEC  // measurement builds: 0 keeps bf16's conv2 on conv_ws_dma_kernel
+#define ABD_BF16_SPEC 1
+#endif
+template <int EPI, int NJ = 2, int NP = 3>
 __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
-  constexpr int NP = 3, CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, NC = 4, G = CS / 16;
+  static_assert(NP == 3 || (NP == 1 && NJ == 2), "f32split planes, or bf16 planes for conv2");
+  constexpr int CS = 64, N = 32 * NJ, K = 4 * CS, LD = K + 8, WPB = 8, NC = 4, G = CS / 16;
   static_assert(G == 4, "the group parity selects the stage buffer; the producer loads one tile ahead");
   constexpr bool ZROW = EPI != EPI_CONV;
   constexpr int SPOS = kDmaSpan + (ZROW ? 1 : 0);
@@ -2770,12 +2778,21 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
   };
   if (producer) {
     // ---- producer: group q + 1 into buffer (q + 1) & 1 while the consumer reads group q ----
-    const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.src), 0, (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
+    const __amdgpu_buffer_rsrc_t arsrc =
+        NP == 1 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.srcs), 0,
+                                                    (int)std::min<int64_t>((int64_t)npos * CS * 2, 0x7ffffff0), 0x00020000)
+                : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.src), 0,
+                                                    (int)std::min<int64_t>((int64_t)npos * CS * 4, 0x7ffffff0), 0x00020000);
     auto fetch = [&](int p0, int cg, int need, float4 (&r)[2][2]) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int pos = (lane & 31) + 32 * k, h = lane >> 5;
+        if constexpr (NP == 1) {  // 8 bf16 channels of the plane: one 16-B load (r[k][1] unused)
+          const uint32_t off = pos < need ? (uint32_t)(((p0 + pos) * CS + cg * 16 + h * 8) * 2) : kOOB;
+          r[k][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)off, 0, 0));
+          r[k][1] = r[k][0];
+          continue;
+        }
         const uint32_t off = pos < need ? (uint32_t)(((p0 + pos) * CS + cg * 16 + h * 8) * 4) : kOOB;
         if constexpr ((ABD_SPEC_ABL & 2) != 0) {
           typedef float fv4 __attribute__((ext_vector_type(4)));
@@ -2803,6 +2820,10 @@ __global__ void __launch_bounds__(512, 1) conv_ws_spec_kernel(NTArgs a) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int pos = (lane & 31) + 32 * k, h = lane >> 5;
+        if constexpr (NP == 1) {
+          *reinterpret_cast<bf16x8*>(sw + pos * kPreRow + h * 8) = __builtin_bit_cast(bf16x8, r[k][0]);
+          continue;
+        }
         bf16x8 pl[NP];
         planes_x8<NP>(r[k][0], r[k][1], pl);
 #pragma unroll
@@ -4373,7 +4394,7 @@ WsKind ws_kind(const NTArgs& a) {
   if ((!PA || NP == 1) && dma && (a.N == 64 || (a.N == 32 && !PA)) && a.Cs == 64 &&
       (EPI == EPI_CONV ? fwd_taps : (EPI == EPI_STORE && dg_taps)) && dma_span(a) <= kDmaSpan) {
     constexpr bool spec = ABD_WS_SPEC >= 2 || (ABD_WS_SPEC == 1 && EPI == EPI_CONV);
-    if (PA && NP == 1) return WS_DMA;
+    if (PA && NP == 1) return ABD_BF16_SPEC ? WS_SPEC : WS_DMA;
     if (NP == 3 && a.N == 64 && ABD_WS_PRE) return spec ? WS_SPEC : WS_PRE;
     if (NP == 3 && a.N == 32 && ABD_WS_PRE >= 3) return spec ? WS_SPEC : WS_PRE;
     return WS_DMA;
@@ -4400,8 +4421,10 @@ int launch_conv_ws_split(const NTArgs& a, hipStream_t s, int phase) {
   // the direct kernel by default (ws_dma_mode); bf16's plane-operand data gradient is staged
   // (0.0702 -> 0.0683 ms).  conv3 (N = 32) runs the same kernels with one 32-column tile per wave.
   if (kind != WS_SPLIT) {
-    if constexpr (PA && NP == 1) conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
-    else if (kind == WS_SPEC && a.N == 64) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
+    if constexpr (PA && NP == 1) {
+      if (kind == WS_SPEC) conv_ws_spec_kernel<EPI, 2, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
+      else conv_ws_dma_kernel<EPI, 1, 2, true><<<dim3(nb), dim3(512), 0, s>>>(a);
+    } else if (kind == WS_SPEC && a.N == 64) conv_ws_spec_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (kind == WS_SPEC) conv_ws_spec_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (kind == WS_PRE && a.N == 64) conv_ws_pre_kernel<EPI><<<dim3(nb), dim3(512), 0, s>>>(a);
     else if (kind == WS_PRE) conv_ws_pre_kernel<EPI, 1><<<dim3(nb), dim3(512), 0, s>>>(a);

@@ -25,7 +25,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-WATCH = (("conv2 dgrad", "conv_ws_spec_kernel<0, 2>"), ("conv2 wgrad", "conv_wgrad_trp_kernel<6, 64"),
+WATCH = (("conv2 dgrad", "conv_ws_spec_kernel<0, 2"), ("conv2 wgrad", "conv_wgrad_trp_kernel<6, 64"),
          ("head_dgrad", "head_dgrad_kernel"), ("head_bwd", "head_bwd_kernel"),
          ("conv1 wgrad", "conv1_wgrad_kernel"), ("adam", "adam_kernel"),
          ("bn2 bwd apply", "bn_bwd_apply_kernel"), ("conv3 wgrad", "conv_wgrad_trp_kernel<4, 32"))

@@ -10,7 +10,7 @@ import sys
 
 run, out = sys.argv[1], sys.argv[2]
 KERNELS = {
-    "conv": ["conv_ws_spec_kernel<1, 2>", "conv_ws_spec_kernel<0, 2>", "conv_ws_spec_kernel<1, 1>",
+    "conv": ["conv_ws_spec_kernel<1, 2", "conv_ws_spec_kernel<0, 2", "conv_ws_spec_kernel<1, 1",
              "conv_ws_pre_kernel<1, 2>", "conv_ws_pre_kernel<0, 2>", "conv_ws_pre_kernel<1, 1>",
              "conv_ws_dma_kernel<1, 3, 2", "conv_ws_split_kernel<0, 2, 64", "conv_wgrad_trp_kernel<6, 64",
              "conv_ws_dma_kernel<1, 3, 1", "conv_ws_split_kernel<0, 2, 32", "conv_wgrad_trp_kernel<4, 32",

@@ -32,7 +32,7 @@ PHASE_KERNELS = {
                  ("stft_mel_fast_kernel<2304, 1103, 16, 12, 12, 1, true>", 0)],
     "db_dct": [("db_dct_mfma_kernel<3>", 0)],
     "conv1_stats": [("conv1_stats_fold_kernel", 0), ("conv1_stats_kernel", 0)],
-    "conv2_fwd": [("conv_ws_spec_kernel<1, 2>", 0), ("conv_ws_pre_kernel<1, 2>", 0), ("conv_ws_dma_kernel<1, 3, 2, false>", 0),
+    "conv2_fwd": [("conv_ws_spec_kernel<1, 2, 3>", 0), ("conv_ws_spec_kernel<1, 2, 1>", 0), ("conv_ws_spec_kernel<1, 2>", 0), ("conv_ws_pre_kernel<1, 2>", 0), ("conv_ws_dma_kernel<1, 3, 2, false>", 0),
                   ("conv_ws_dma_kernel<1, 1, 2, true>", 0), ("conv_ws_dma_kernel<1, 3, 2>", 0), ("conv_ws_dma_kernel<1, 1, 2>", 0),
                   ("conv_ws_dma_kernel<1, 3>", 0), ("conv_ws_dma_kernel<1, 1>", 0),
                   ("conv_ws_dma_kernel<3>", 0), ("conv_ws_dma_kernel<1>", 0),
@@ -42,7 +42,7 @@ PHASE_KERNELS = {
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, true>", 0),
                   ("conv_ws_split_kernel<1, 2, 64, 1, 8, 8, 1, false>", 0)],
     "bn2_pool": [("bn_pool_fwd_kernel", 0)],
-    "conv3_fwd": [("conv_ws_spec_kernel<1, 1>", 0), ("conv_ws_pre_kernel<1, 1>", 0), ("conv_ws_dma_kernel<1, 3, 1, false>", 0),
+    "conv3_fwd": [("conv_ws_spec_kernel<1, 1, 3>", 0), ("conv_ws_spec_kernel<1, 1>", 0), ("conv_ws_pre_kernel<1, 1>", 0), ("conv_ws_dma_kernel<1, 3, 1, false>", 0),
                   ("conv_ws_dma_kernel<1, 1, 1, false>", 0), ("conv_ws_dma_kernel<1, 3, 1>", 0), ("conv_ws_dma_kernel<1, 1, 1>", 0),
                   ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 3, false, true>", 0),
                   ("conv_ws_split_kernel<1, 1, 64, 1, 4, 8, 1, false, true>", 0),
@@ -66,7 +66,7 @@ PHASE_KERNELS = {
                     ("conv_ws_split_kernel<0, 2, 32, 1, 4, 8, 1, false>", 0)],
     "conv2_wgrad": [("conv_wgrad_trp_kernel<6, 64, 5, 11, 3, false>", 0),
                     ("conv_wgrad_trp_kernel<6, 64, 5, 11, 1, true>", 0)],
-    "conv2_dgrad": [("conv_ws_spec_kernel<0, 2>", 0), ("conv_ws_pre_kernel<0, 2>", 0), ("conv_ws_dma_kernel<0, 1, 2, true>", 0),
+    "conv2_dgrad": [("conv_ws_spec_kernel<0, 2, 3>", 0), ("conv_ws_spec_kernel<0, 2, 1>", 0), ("conv_ws_spec_kernel<0, 2>", 0), ("conv_ws_pre_kernel<0, 2>", 0), ("conv_ws_dma_kernel<0, 1, 2, true>", 0),
                     ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false, false>", 0),
                     ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 1, true, false>", 0),
                     ("conv_ws_split_kernel<0, 2, 64, 1, 8, 8, 3, false>", 0),
