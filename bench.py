@@ -31,6 +31,7 @@ BF16_PHASES = ("conv2_fwd", "conv2_dgrad", "conv3_fwd", "conv3_dgrad", "conv2_wg
 SPLIT_TERMS = 6                 # f32split: six bf16 MFMA terms per fp32-accurate product
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (vector) 157.3 TF
+VALU_CLOCK_GHZ = 2.4  # peak engine clock: one wave64 VALU issue per CU-cycle (non-packed)
 
 
 def algorithmic_work(phase, B, H0, W0, K, n_mels, T, C, L):
@@ -134,6 +135,15 @@ def traffic_file():
                 break
         _TRAFFIC.append(found)
     return _TRAFFIC[0]
+
+
+def load_valu_insts(phase):
+    """(VALU wave-instructions per launch, source file) for a phase from the same-source traffic file's
+    SQ_INSTS_VALU pass, else (None, None)."""
+    tf = traffic_file()
+    if tf is None or phase not in tf[1].get("valu_insts_per_launch", {}):
+        return None, None
+    return tf[1]["valu_insts_per_launch"][phase], tf[0]
 
 
 def load_traffic(phase):
@@ -590,6 +600,19 @@ def main():
                                                "frac": round(tf / FP32_VECTOR_PEAK_TFLOPS, 4),
                                                "ms": round(pms / pcnt, 4),
                                                "formula": "B * ceil(T/2) pairs * 2 FFTs * 5 M log2 M, M = 2304"}
+                # and against the VALU issue limit: one wave64 VALU instruction per CU-cycle without
+                # packed FP32 (4 SIMDs x 16 lanes; MI355X_MICROARCH.md), instructions counted by the
+                # same-source SQ_INSTS_VALU pass
+                vi, vsrc = load_valu_insts("stft_mel") if headline else (None, None)
+                if vi:
+                    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+                    gi = vi / (pms / pcnt / 1e3) / 1e9
+                    pk = ncu * VALU_CLOCK_GHZ
+                    per_kernel["stft_mel_issue"] = {"bound": "valu_issue", "achieved": round(gi, 1),
+                                                    "unit": "G wave-instr/s", "peak": round(pk, 1),
+                                                    "frac": round(gi / pk, 4), "ms": round(pms / pcnt, 4),
+                                                    "valu_insts_per_launch": vi, "source": vsrc,
+                                                    "formula": "SQ_INSTS_VALU per launch / launch time vs CUs x 2.4 GHz"}
         cpu = None
         if world == 1 and not args.no_cpu and args.cpu_train > 0 and args.attack == "ultrasonic":
             cpu = cpu_baseline(args.batch, cpu_threads(), n_train=args.cpu_train)

@@ -13,5 +13,6 @@ cp "$O/smoke.log" "${P}_smoke.txt"
 cp "$O/kt/kt_kernel_stats.csv" "${P}_kernel_stats.csv"
 [ -f "$O/configs.jsonl" ] && cp "$O/configs.jsonl" "${P}_configs.jsonl"
 [ -f "$O/bench_dp2_gloo.json" ] && cp "$O/bench_dp2_gloo.json" "${P}_bench_dp2_gloo_rehearsal.json"
+if [ -d "$O/p_sq" ]; then mkdir -p "${P}_sq_pmc" && cp "$O"/p_sq/*counter_collection.csv "$O"/p_sq/*agent_info.csv "${P}_sq_pmc/"; fi
 python scripts/traffic_json.py "$O" "${P}_traffic.json"
 echo "collected $T"

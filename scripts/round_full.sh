@@ -35,7 +35,7 @@ step pmc-fetch
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/p_fetch" -o p -f csv -- $CMD > "$O/p_fetch.log" 2>&1 || { tail -20 "$O/p_fetch.log"; exit 1; }
 step pmc-write
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$O/p_write" -o p -f csv -- $CMD > "$O/p_write.log" 2>&1 || { tail -20 "$O/p_write.log"; exit 1; }
-if [ "${SQ_PMC:-0}" = 1 ]; then
+if [ "${SQ_PMC:-1}" = 1 ]; then
   step pmc-sq
   timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
     -d "$O/p_sq" -o p -f csv -- $CMD > "$O/p_sq.log" 2>&1 || { tail -20 "$O/p_sq.log"; exit 1; }

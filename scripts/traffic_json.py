@@ -153,6 +153,15 @@ def main():
         rb, wb = 2 * f[2] * 1024, w[2] * 1024
         res["bytes_per_launch"][ph] = round(rb + wb)
         res["detail"][ph] = {"kernel": f[0], "occurrence": f[1], "read_bytes": round(rb), "write_bytes": round(wb)}
+    # VALU wave-instructions per launch (summed over the chip), when the run has an SQ_INSTS_VALU pass
+    # (round_full.sh's p_sq): bench.py prices stft_mel against the VALU issue limit with it
+    valu = last_step(d, "SQ_INSTS_VALU")
+    if valu:
+        res["valu_insts_per_launch"] = {}
+        for ph, cands in PHASE_KERNELS.items():
+            v = pick(valu, cands)
+            if v is not None:
+                res["valu_insts_per_launch"][ph] = round(v[2])
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res["bytes_per_launch"]))
 
