@@ -590,6 +590,10 @@ def main():
             tb, tsrc = load_traffic(ph) if headline else (None, None)
             per_kernel[ph] = {"bound": bnd, "achieved": round(ach, 2), "unit": unit, "peak": pk, "frac": round(ach / pk, 4),
                               "ms": round(pms / pcnt, 4), "traffic": tb, "traffic_source": tsrc}
+            vi, _ = load_valu_insts(ph) if headline else (None, None)
+            if vi:  # VALU issue rate against one wave64 instruction per CU-cycle (same-source SQ pass)
+                ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+                per_kernel[ph]["valu_issue_frac"] = round(vi / (pms / pcnt / 1e3) / (ncu * VALU_CLOCK_GHZ * 1e9), 4)
             if ph == "stft_mel" and cfg.n_fft == 1103:
                 # the limiter the byte model misses: the Bluestein FFTs' arithmetic
                 # (5 M log2 M per complex M-point FFT, two per frame pair) against the fp32 VECTOR
